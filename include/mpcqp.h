@@ -1,0 +1,155 @@
+/*
+ * mpcqp.h -- C-ABI of the MI355X batched bicycle-MPC QP solver (libmpcqp.so).
+ *
+ * Drop-in boundary for the reference's MPC hot path (CagriCatik/RRT-MPC):
+ *
+ *   reference call                                         replaced by
+ *   -----------------------------------------------------  -----------------------------
+ *   src/control/mpc_controller.py:17-30  MPCParameters      mpcqp_params (+ solver settings
+ *                                                          of mpc_controller.py:121-131)
+ *   src/control/mpc_controller.py:59-70  unwrap + N x       mpcqp_build   (HIP kernel K1)
+ *   src/control/vehicle_model.py:24-45   linearize()
+ *   src/control/mpc_controller.py:53-117 cvxpy assembly +   mpcqp_solve   (HIP kernel K2)
+ *   src/control/mpc_controller.py:119-132 OSQP solve
+ *   src/control/mpc_controller.py:133-141 status / return   status[] codes below
+ *
+ * The reference binds this path from Python; the ctypes binding lives in
+ * rrt-mpc_amd/mpcqp/_lib.py and INTEGRATION.md shows the reference-side stub.
+ *
+ * Conventions
+ *  - All numeric I/O is IEEE float64, row-major, contiguous, caller-owned DEVICE
+ *    memory (e.g. torch.cuda tensors); the library never frees caller buffers.
+ *  - Calls are asynchronous on the given hipStream_t (NULL = default stream).
+ *  - Return value: 0 on success, a negative MPCQP_E_* code otherwise; no C++
+ *    exception crosses the ABI.  mpcqp_last_error() describes the last failure
+ *    of the calling thread.
+ *  - Re-entrant across distinct workspaces; NOT thread-safe on one workspace.
+ *  - One workspace is bound to one device; use one process per GPU.
+ */
+#ifndef MPCQP_H
+#define MPCQP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MPCQP_ABI_VERSION 1
+
+/* error codes (function return values) */
+#define MPCQP_OK 0
+#define MPCQP_E_ARG (-1)         /* bad pointer / size / parameter */
+#define MPCQP_E_HORIZON (-2)     /* horizon outside [1, MPCQP_MAX_HORIZON] */
+#define MPCQP_E_BATCH (-3)       /* B > max_batch of the workspace */
+#define MPCQP_E_HIP (-4)         /* HIP runtime / launch error */
+#define MPCQP_E_STATE (-5)       /* mpcqp_solve before mpcqp_build of the same B */
+
+#define MPCQP_MAX_HORIZON 31     /* 2N+1 <= 64: one QP per 64-lane wavefront */
+
+/* per-QP status codes (mirror OSQP's; mpc_controller.py:137 accepts 1 and 2) */
+#define MPCQP_SOLVED 1            /* polish converged: exact optimum (active set reproduces itself) */
+#define MPCQP_SOLVED_INACCURATE 2 /* ADMM met eps_abs/eps_rel but polish did not converge */
+#define MPCQP_MAX_ITER_REACHED (-2)
+#define MPCQP_NUMERICAL_ERROR (-10) /* non-finite data or non-positive pivot */
+
+/* active[] codes per soft row */
+#define MPCQP_ROW_INACTIVE 0
+#define MPCQP_ROW_LOWER 1         /* row value below its lower bound (slack > 0) */
+#define MPCQP_ROW_UPPER 2         /* row value above its upper bound (slack > 0) */
+
+/* solve methods */
+#define MPCQP_METHOD_ADMM 0       /* OSQP algorithm: Ruiz scaling, ADMM, adaptive rho, polish */
+#define MPCQP_METHOD_NEWTON 1     /* polish iteration only (semismooth Newton from the unconstrained optimum) */
+
+/*
+ * Parameter block.  Mirrors MPCParameters (mpc_controller.py:17-30) and the
+ * OSQP settings of mpc_controller.py:121-131.  Matrices are row-major.
+ */
+typedef struct mpcqp_params {
+  int32_t horizon;            /* N */
+  int32_t method;             /* MPCQP_METHOD_* */
+  double wheelbase_px;        /* L (config.py:79-81: wheelbase_m / map_resolution) */
+  double dt;
+  double q[16];               /* Q   (4x4) stage state weight, quad_form without 1/2 */
+  double r[4];                /* R   (2x2) input weight */
+  double q_terminal[16];      /* Q_N (4x4) */
+  double u_bounds[4];         /* {a_lo, a_hi, delta_lo, delta_hi} */
+  double v_bounds[2];         /* {v_lo, v_hi} */
+  double du_bounds[4];        /* {da_lo, da_hi, ddelta_lo, ddelta_hi} */
+  double slack_velocity;      /* w_v  (default 1e3) */
+  double slack_input;         /* w_u  (default 5e2) */
+  double slack_rate;          /* w_du (default 5e2) */
+  /* solver settings */
+  double rho;                 /* 0.1 */
+  double sigma;               /* 1e-6 (OSQP default) */
+  double alpha;               /* 1.6 */
+  double eps_abs;             /* 1e-3 */
+  double eps_rel;             /* 1e-3 */
+  double adaptive_rho_tolerance; /* 5 (OSQP default) */
+  int32_t max_iter;           /* 60000 */
+  int32_t check_termination;  /* 25 (OSQP default) */
+  int32_t scaling;            /* 10 Ruiz iterations (OSQP default) */
+  int32_t adaptive_rho;       /* 1 */
+  int32_t adaptive_rho_interval; /* 25 (deterministic; OSQP's default is timing based) */
+  int32_t polish;             /* 1 */
+  int32_t polish_max_iter;    /* 100 */
+  int32_t reserved;
+} mpcqp_params;
+
+typedef struct mpcqp_ws mpcqp_ws;
+
+/* ABI version (MPCQP_ABI_VERSION). */
+int mpcqp_version(void);
+
+/* Thread-local description of the last error ("" if none). */
+const char* mpcqp_last_error(void);
+
+/* Number of soft rows per QP: 5N+1 (v rows 0..N, input rows, rate rows). */
+int mpcqp_num_rows(int horizon);
+
+/* Workspace of capacity max_batch QPs on HIP device `device`.
+ * Replaces the per-call cvxpy Problem construction (mpc_controller.py:53-119). */
+int mpcqp_create(const mpcqp_params* p, int max_batch, int device, mpcqp_ws** ws);
+
+/* Replace the parameter block (same horizon), e.g. for the relaxation retry of
+ * control_stage.py:45-55.  Stream-ordered with respect to later launches. */
+int mpcqp_set_params(mpcqp_ws* ws, const mpcqp_params* p);
+
+void mpcqp_destroy(mpcqp_ws* ws);
+
+/*
+ * K1: window -> LTV model.  Per QP: np.unwrap of the reference yaw
+ * (mpc_controller.py:59-60, numpy semantics) and the N Jacobians of
+ * linearize() at ref[max(k-1,0)], u=0 (mpc_controller.py:65-70,108;
+ * vehicle_model.py:24-45).  Inputs (device):
+ *   x0     B x 4
+ *   ref    B x (N+1) x 4     [x, y, yaw, v] per row, as ref_traj of solve()
+ *   u_prev B x 2             (NULL = zeros, mpc_controller.py:48-49)
+ */
+int mpcqp_build(mpcqp_ws* ws, int B, const double* x0, const double* ref, const double* u_prev,
+                void* stream);
+
+/*
+ * K2: condense + (ADMM + polish | Newton) for the B QPs of the last build.
+ * Outputs (device, any may be NULL except status):
+ *   u0     B x 2             U[:,0]  (mpc_controller.py:141)
+ *   X      B x 4 x (N+1)     predicted states, X[:,0] = x0
+ *   U      B x 2 x N         inputs
+ *   status B                 MPCQP_SOLVED / ... per QP
+ *   iters  B x 2             {ADMM iterations, polish iterations}
+ *   active B x (5N+1)        MPCQP_ROW_* per soft row at the returned solution
+ */
+int mpcqp_solve(mpcqp_ws* ws, int B, double* u0, double* X, double* U, int32_t* status,
+                int32_t* iters, uint8_t* active, void* stream);
+
+/* Workspace device buffer holding the K1 output (for tests / inspection):
+ * B x mpcqp_model_stride(N) doubles, layout documented in DESIGN.md. */
+const double* mpcqp_model_buffer(const mpcqp_ws* ws);
+int mpcqp_model_stride(int horizon);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* MPCQP_H */

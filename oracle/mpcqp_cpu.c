@@ -1,0 +1,679 @@
+/*
+ * mpcqp_cpu.c -- CPU restatement of the batched MPC QP solve (ORACLE / CPU BASELINE).
+ *
+ * TEST INFRASTRUCTURE ONLY: linked by tests/ and by bench.py's cpu_baseline
+ * leg (the "CPU OSQP path timed beside the GPU"), never by the
+ * product library.  It runs, sequentially per QP (OpenMP over the batch), the
+ * same algorithm as the HIP kernels in rrt-mpc_amd/csrc/mpcqp.hip:
+ *
+ *   build   : np.unwrap of ref yaw (numpy semantics)      mpc_controller.py:59-60
+ *             linearize() at ref[max(k-1,0)], u = 0       mpc_controller.py:65-70,108
+ *                                                         vehicle_model.py:24-45
+ *   condense: states and slacks eliminated; the QP of      mpc_controller.py:53-117
+ *             mpc_controller.py becomes min U'HU+2g'U+sum w dist(CU+b,[lo,hi])^2
+ *   solve   : OSQP's algorithm with the reference settings (mpc_controller.py:121-131):
+ *             Ruiz scaling (10 it) + cost scaling, ADMM (rho 0.1, sigma 1e-6,
+ *             alpha 1.6), adaptive rho, eps_abs = eps_rel = 1e-3 termination;
+ *             the projection onto [l,u] is the prox of w*dist^2 (slacks eliminated);
+ *             then polish = semismooth-Newton active-set iteration until the
+ *             active set reproduces itself (exact optimum).
+ *
+ * Parity of this file's *solutions* is pinned against oracle/mpc_oracle.py's exact
+ * solve (tests/test_oracle.py); it is the reference implementation for the GPU's
+ * iteration counts.
+ */
+#include <math.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+
+#include "../include/mpcqp.h"
+
+#define MAXN MPCQP_MAX_HORIZON
+#define MAXNV (2 * MAXN)
+#define MAXR (5 * MAXN)
+#define PI_D 3.141592653589793
+#define TWO_PI_D 6.283185307179586
+#define MIN_SCALING 1e-4
+#define MAX_SCALING 1e4
+#define RHO_MIN 1e-6
+#define RHO_MAX 1e6
+#define DIV_TOL 1e-30
+
+int mpcqp_model_stride(int N) { return ((11 * N + 10) + 7) / 8 * 8; }
+
+/* numpy float mod (npy_divmod) for b > 0 */
+static double np_mod(double a, double b) {
+  double m = fmod(a, b);
+  if (m != 0.0) {
+    if (m < 0.0) m += b;
+  } else {
+    m = 0.0;
+  }
+  return m;
+}
+
+/* ---------------------------------------------------------------- build */
+void mpcqp_cpu_build_one(const mpcqp_params* p, const double* x0, const double* ref, const double* u_prev,
+                         double* model) {
+  const int N = p->horizon;
+  double* al = model;
+  double* be = model + N;
+  double* ga = model + 2 * N;
+  double* et = model + 3 * N;
+  double* si = model + 4 * N;
+  double* c0 = model + 5 * N;
+  double* c1 = model + 6 * N;
+  double* r = model + 7 * N;
+  double* mx0 = model + 11 * N + 4;
+  double* mup = model + 11 * N + 8;
+  /* np.unwrap(ref[:,2]) */
+  double cs = 0.0;
+  for (int k = 0; k <= N; ++k) {
+    r[4 * k + 0] = ref[4 * k + 0];
+    r[4 * k + 1] = ref[4 * k + 1];
+    r[4 * k + 3] = ref[4 * k + 3];
+    if (k == 0) {
+      r[2] = ref[2];
+      continue;
+    }
+    double dd = ref[4 * k + 2] - ref[4 * (k - 1) + 2];
+    double ddmod = np_mod(dd + PI_D, TWO_PI_D) + (-PI_D);
+    if (ddmod == -PI_D && dd > 0.0) ddmod = PI_D;
+    double pc = ddmod - dd;
+    if (fabs(dd) < PI_D) pc = 0.0;
+    cs = cs + pc;
+    r[4 * k + 2] = ref[4 * k + 2] + cs;
+  }
+  const double dt = p->dt, L = p->wheelbase_px;
+  const double sec2 = 1.0 / (1.0 * 1.0 + 1e-9); /* 1/(cos(0)^2 + 1e-9) */
+  for (int k = 0; k < N; ++k) {
+    const int kk = k == 0 ? 0 : k - 1;
+    const double psi = r[4 * kk + 2], v = r[4 * kk + 3];
+    const double s = sin(psi), c = cos(psi);
+    al[k] = -dt * v * s;
+    be[k] = dt * c;
+    ga[k] = dt * v * c;
+    et[k] = dt * s;
+    si[k] = dt * (v / L) * sec2;
+    c0[k] = -al[k] * psi; /* fx - A xbar, row 0 (analytically dt v psi sin psi) */
+    c1[k] = -ga[k] * psi; /* row 1 */
+  }
+  for (int i = 0; i < 4; ++i) mx0[i] = x0[i];
+  mup[0] = u_prev ? u_prev[0] : 0.0;
+  mup[1] = u_prev ? u_prev[1] : 0.0;
+}
+
+/* ---------------------------------------------------------------- solver state */
+typedef struct {
+  int N, n, m; /* m = 5N ADMM rows: v rows 1..N [0,N), u rows [N,3N), du rows [3N,5N) */
+  double H[MAXNV][MAXNV];
+  double g[MAXNV];
+  double P[MAXNV][MAXNV]; /* scaled P-bar */
+  double q[MAXNV];
+  double D[MAXNV], E[MAXR], c;
+  double l[MAXR], u[MAXR], w[MAXR]; /* scaled bounds and prox weights */
+  double dt;
+  double K[MAXNV][MAXNV]; /* inverse workspace */
+  double M[MAXNV][MAXNV];
+} qp_t;
+
+static inline double limit_scaling(double v) {
+  if (v < MIN_SCALING) return 1.0;
+  if (v > MAX_SCALING) return MAX_SCALING;
+  return v;
+}
+
+/* z = Cbar x  (structured: v rows prefix sums, u rows identity, du rows differences) */
+static void Cmul(const qp_t* s, const double* x, double* z) {
+  const int N = s->N, n = s->n;
+  double acc = 0.0;
+  for (int j = 0; j < N; ++j) {
+    acc += s->D[2 * j] * x[2 * j];
+    z[j] = s->E[j] * s->dt * acc; /* v row j+1 */
+  }
+  for (int p = 0; p < n; ++p) {
+    z[N + p] = s->E[N + p] * (s->D[p] * x[p]);
+    double d = s->D[p] * x[p];
+    if (p >= 2) d -= s->D[p - 2] * x[p - 2];
+    z[3 * N + p] = s->E[3 * N + p] * d;
+  }
+}
+
+/* x = Cbar' y */
+static void CTmul(const qp_t* s, const double* y, double* x) {
+  const int N = s->N, n = s->n;
+  double suf = 0.0;
+  for (int j = N - 1; j >= 0; --j) {
+    suf += s->E[j] * y[j];
+    x[2 * j] = s->dt * suf;
+    x[2 * j + 1] = 0.0;
+  }
+  for (int p = 0; p < n; ++p) {
+    double t = x[p] + s->E[N + p] * y[N + p] + s->E[3 * N + p] * y[3 * N + p];
+    if (p + 2 < n) t -= s->E[3 * N + p + 2] * y[3 * N + p + 2];
+    x[p] = s->D[p] * t;
+  }
+}
+
+/* A = Pbar + sig I + Cbar' diag(rw) Cbar  (rw per ADMM row) */
+static void form_kkt(const qp_t* s, double sig, const double* rw, double A[MAXNV][MAXNV]) {
+  const int N = s->N, n = s->n;
+  double Sv[MAXN + 2];
+  Sv[N] = 0.0;
+  for (int j = N - 1; j >= 0; --j) Sv[j] = Sv[j + 1] + s->E[j] * s->E[j] * rw[j]; /* sum over v rows k>=j+1 */
+  for (int i = 0; i < n; ++i) {
+    for (int j = 0; j < n; ++j) {
+      double t = 0.0;
+      if ((i & 1) == 0 && (j & 1) == 0) {
+        int mx = (i > j ? i : j) / 2;
+        t = s->dt * s->dt * Sv[mx];
+      }
+      if (i == j) {
+        t += s->E[N + i] * s->E[N + i] * rw[N + i] + s->E[3 * N + i] * s->E[3 * N + i] * rw[3 * N + i];
+        if (i + 2 < n) t += s->E[3 * N + i + 2] * s->E[3 * N + i + 2] * rw[3 * N + i + 2];
+      } else if (j == i + 2) {
+        t -= s->E[3 * N + j] * s->E[3 * N + j] * rw[3 * N + j];
+      } else if (i == j + 2) {
+        t -= s->E[3 * N + i] * s->E[3 * N + i] * rw[3 * N + i];
+      }
+      A[i][j] = s->P[i][j] + s->D[i] * s->D[j] * t + (i == j ? sig : 0.0);
+    }
+  }
+}
+
+/* in-place symmetric sweep: A <- A^{-1} (SPD, no pivoting).  returns 0 / -1 on bad pivot */
+static int sweep_inverse(int n, double A[MAXNV][MAXNV]) {
+  for (int k = 0; k < n; ++k) {
+    const double d = A[k][k];
+    if (!(d > 0.0) || !isfinite(d)) return -1;
+    const double inv = 1.0 / d;
+    double col[MAXNV];
+    for (int i = 0; i < n; ++i) col[i] = A[i][k];
+    for (int i = 0; i < n; ++i) {
+      if (i == k) continue;
+      const double f = col[i] * inv;
+      for (int j = 0; j < n; ++j) {
+        if (j == k) continue;
+        A[i][j] -= f * col[j];
+      }
+      A[i][k] = f;
+    }
+    for (int j = 0; j < n; ++j) A[k][j] = col[j] * inv;
+    A[k][k] = -inv;
+  }
+  /* A now holds -A^{-1} */
+  for (int i = 0; i < n; ++i)
+    for (int j = 0; j < n; ++j) A[i][j] = -A[i][j];
+  return 0;
+}
+
+static void matvec(int n, double A[MAXNV][MAXNV], const double* x, double* y) {
+  for (int i = 0; i < n; ++i) {
+    double t = 0.0;
+    for (int j = 0; j < n; ++j) t += A[i][j] * x[j];
+    y[i] = t;
+  }
+}
+
+static double vmaxabs(int n, const double* x) {
+  double m = 0.0;
+  for (int i = 0; i < n; ++i) m = fmax(m, fabs(x[i]));
+  return m;
+}
+
+/* condensed H, g from the LTV model (backward adjoint recursion per column) */
+static void condense(const mpcqp_params* p, const double* model, qp_t* s) {
+  const int N = p->horizon, n = 2 * N;
+  const double* al = model;
+  const double* be = model + N;
+  const double* ga = model + 2 * N;
+  const double* et = model + 3 * N;
+  const double* si = model + 4 * N;
+  const double* c0 = model + 5 * N;
+  const double* c1 = model + 6 * N;
+  const double* r = model + 7 * N;
+  const double* x0 = model + 11 * N + 4;
+  const double dt = p->dt;
+  double Q[4][4], QN[4][4], R[2][2];
+  for (int i = 0; i < 4; ++i)
+    for (int j = 0; j < 4; ++j) {
+      Q[i][j] = 0.5 * (p->q[4 * i + j] + p->q[4 * j + i]);
+      QN[i][j] = 0.5 * (p->q_terminal[4 * i + j] + p->q_terminal[4 * j + i]);
+    }
+  for (int i = 0; i < 2; ++i)
+    for (int j = 0; j < 2; ++j) R[i][j] = 0.5 * (p->r[2 * i + j] + p->r[2 * j + i]);
+  double Pa[MAXN + 1], Pb[MAXN + 1], Pg[MAXN + 1], Pe[MAXN + 1];
+  Pa[0] = Pb[0] = Pg[0] = Pe[0] = 0.0;
+  for (int k = 0; k < N; ++k) {
+    Pa[k + 1] = Pa[k] + al[k];
+    Pb[k + 1] = Pb[k] + be[k];
+    Pg[k + 1] = Pg[k] + ga[k];
+    Pe[k + 1] = Pe[k] + et[k];
+  }
+  /* free response error e_m = sx_m - r_m */
+  double e[MAXN + 1][4];
+  {
+    double px = x0[0], py = x0[1];
+    const double psi = x0[2], v = x0[3];
+    for (int m = 1; m <= N; ++m) {
+      const int k = m - 1;
+      px = px + al[k] * psi + be[k] * v + c0[k];
+      py = py + ga[k] * psi + et[k] * v + c1[k];
+      e[m][0] = px - r[4 * m + 0];
+      e[m][1] = py - r[4 * m + 1];
+      e[m][2] = psi - r[4 * m + 2];
+      e[m][3] = v - r[4 * m + 3];
+    }
+  }
+  for (int col = 0; col <= n; ++col) {
+    const int j = col >> 1, c = col & 1;
+    double mu[4] = {0, 0, 0, 0};
+    for (int m = N; m >= 1; --m) {
+      double sv[4];
+      if (col == n) {
+        sv[0] = e[m][0];
+        sv[1] = e[m][1];
+        sv[2] = e[m][2];
+        sv[3] = e[m][3];
+      } else if (m > j) {
+        if (c == 0) {
+          sv[0] = dt * (Pb[m] - Pb[j + 1]);
+          sv[1] = dt * (Pe[m] - Pe[j + 1]);
+          sv[2] = 0.0;
+          sv[3] = dt;
+        } else {
+          sv[0] = si[j] * (Pa[m] - Pa[j + 1]);
+          sv[1] = si[j] * (Pg[m] - Pg[j + 1]);
+          sv[2] = si[j];
+          sv[3] = 0.0;
+        }
+      } else {
+        sv[0] = sv[1] = sv[2] = sv[3] = 0.0;
+      }
+      double (*W)[4] = (m == N) ? QN : Q;
+      double ws[4];
+      for (int a = 0; a < 4; ++a) ws[a] = W[a][0] * sv[0] + W[a][1] * sv[1] + W[a][2] * sv[2] + W[a][3] * sv[3];
+      if (m < N) {
+        const double m0 = mu[0], m1 = mu[1];
+        mu[0] = ws[0] + m0;
+        mu[1] = ws[1] + m1;
+        mu[2] = ws[2] + (mu[2] + al[m] * m0 + ga[m] * m1);
+        mu[3] = ws[3] + (mu[3] + be[m] * m0 + et[m] * m1);
+      } else {
+        mu[0] = ws[0];
+        mu[1] = ws[1];
+        mu[2] = ws[2];
+        mu[3] = ws[3];
+      }
+      const double ha = dt * mu[3], hd = si[m - 1] * mu[2];
+      if (col == n) {
+        s->g[2 * (m - 1)] = ha;
+        s->g[2 * (m - 1) + 1] = hd;
+      } else {
+        s->H[2 * (m - 1)][col] = ha;
+        s->H[2 * (m - 1) + 1][col] = hd;
+      }
+    }
+    if (col < n) {
+      s->H[2 * j][col] += R[0][c];
+      s->H[2 * j + 1][col] += R[1][c];
+    }
+  }
+}
+
+/* scaled objective 0.5 x'Px + q'x + sum w dist(Cx,[l,u])^2 given Px */
+static double pen(const qp_t* s, const double* z) {
+  double t = 0.0;
+  for (int r = 0; r < s->m; ++r) {
+    double d = z[r] > s->u[r] ? z[r] - s->u[r] : (z[r] < s->l[r] ? s->l[r] - z[r] : 0.0);
+    t += s->w[r] * d * d;
+  }
+  return t;
+}
+
+static void codes_of(const qp_t* s, const double* z, uint8_t* cd) {
+  for (int r = 0; r < s->m; ++r) cd[r] = z[r] > s->u[r] ? 2 : (z[r] < s->l[r] ? 1 : 0);
+}
+
+/* ---------------------------------------------------------------- one QP */
+void mpcqp_cpu_solve_one(const mpcqp_params* p, const double* model, double* u0, double* Xo, double* Uo,
+                         int32_t* status, int32_t* iters, uint8_t* active) {
+  qp_t S;
+  qp_t* s = &S;
+  const int N = p->horizon, n = 2 * N, m = 5 * N;
+  s->N = N;
+  s->n = n;
+  s->m = m;
+  s->dt = p->dt;
+  const double* al = model;
+  const double* be = model + N;
+  const double* ga = model + 2 * N;
+  const double* et = model + 3 * N;
+  const double* si = model + 4 * N;
+  const double* c0 = model + 5 * N;
+  const double* c1 = model + 6 * N;
+  const double* x0 = model + 11 * N + 4;
+  const double* up = model + 11 * N + 8;
+  int st = MPCQP_MAX_ITER_REACHED;
+  int admm_it = 0, pol_it = 0;
+
+  condense(p, model, s);
+  /* unscaled problem data: P = 2H, q = 2g, bounds with the row offsets folded in */
+  for (int i = 0; i < n; ++i) {
+    s->q[i] = 2.0 * s->g[i];
+    for (int j = 0; j < n; ++j) s->P[i][j] = 2.0 * s->H[i][j];
+  }
+  double lo0[MAXR], hi0[MAXR], w0[MAXR];
+  for (int j = 0; j < N; ++j) {
+    lo0[j] = p->v_bounds[0] - x0[3];
+    hi0[j] = p->v_bounds[1] - x0[3];
+    w0[j] = p->slack_velocity;
+  }
+  for (int q = 0; q < n; ++q) {
+    const int c = q & 1;
+    lo0[N + q] = p->u_bounds[2 * c];
+    hi0[N + q] = p->u_bounds[2 * c + 1];
+    w0[N + q] = p->slack_input;
+    const double off = q < 2 ? up[c] : 0.0; /* du row k=0: U - u_prev */
+    lo0[3 * N + q] = p->du_bounds[2 * c] + off;
+    hi0[3 * N + q] = p->du_bounds[2 * c + 1] + off;
+    w0[3 * N + q] = p->slack_rate;
+  }
+  /* ---- Ruiz equilibration (OSQP scale_data) ---- */
+  for (int i = 0; i < n; ++i) s->D[i] = 1.0;
+  for (int r = 0; r < m; ++r) s->E[r] = 1.0;
+  s->c = 1.0;
+  for (int it = 0; it < p->scaling; ++it) {
+    double dl[MAXNV], el[MAXR];
+    double sufE[MAXN + 1];
+    sufE[N] = 0.0;
+    for (int j = N - 1; j >= 0; --j) sufE[j] = fmax(sufE[j + 1], s->E[j]);
+    for (int q = 0; q < n; ++q) {
+      double cp = 0.0;
+      for (int i = 0; i < n; ++i) cp = fmax(cp, fabs(s->P[i][q]));
+      double cc = fmax(s->E[N + q], s->E[3 * N + q]);
+      if (q + 2 < n) cc = fmax(cc, s->E[3 * N + q + 2]);
+      if ((q & 1) == 0) cc = fmax(cc, s->dt * sufE[q / 2]);
+      cc *= s->D[q];
+      dl[q] = 1.0 / sqrt(limit_scaling(fmax(cp, cc)));
+    }
+    double pre = 0.0;
+    for (int j = 0; j < N; ++j) {
+      pre = fmax(pre, s->D[2 * j]);
+      el[j] = 1.0 / sqrt(limit_scaling(s->E[j] * s->dt * pre));
+    }
+    for (int q = 0; q < n; ++q) {
+      el[N + q] = 1.0 / sqrt(limit_scaling(s->E[N + q] * s->D[q]));
+      double dm = s->D[q];
+      if (q >= 2) dm = fmax(dm, s->D[q - 2]);
+      el[3 * N + q] = 1.0 / sqrt(limit_scaling(s->E[3 * N + q] * dm));
+    }
+    for (int i = 0; i < n; ++i) {
+      s->D[i] *= dl[i];
+      s->q[i] *= dl[i];
+      for (int j = 0; j < n; ++j) s->P[i][j] *= dl[i] * dl[j];
+    }
+    for (int r = 0; r < m; ++r) s->E[r] *= el[r];
+    double cn = 0.0;
+    for (int q = 0; q < n; ++q) {
+      double cp = 0.0;
+      for (int i = 0; i < n; ++i) cp = fmax(cp, fabs(s->P[i][q]));
+      cn += cp;
+    }
+    cn /= n;
+    double ct = 1.0 / limit_scaling(fmax(cn, limit_scaling(vmaxabs(n, s->q))));
+    for (int i = 0; i < n; ++i) {
+      s->q[i] *= ct;
+      for (int j = 0; j < n; ++j) s->P[i][j] *= ct;
+    }
+    s->c *= ct;
+  }
+  for (int r = 0; r < m; ++r) {
+    s->l[r] = s->E[r] * lo0[r];
+    s->u[r] = s->E[r] * hi0[r];
+    s->w[r] = s->c * w0[r] / (s->E[r] * s->E[r]);
+  }
+
+  double x[MAXNV], z[MAXR], y[MAXR];
+  for (int i = 0; i < n; ++i) x[i] = 0.0;
+  for (int r = 0; r < m; ++r) z[r] = y[r] = 0.0;
+  int admm_ok = 0, bad = 0;
+
+  if (p->method == MPCQP_METHOD_ADMM) {
+    double rho = p->rho;
+    const double sig = p->sigma, a = p->alpha;
+    double rw[MAXR];
+    for (int r = 0; r < m; ++r) rw[r] = rho;
+    form_kkt(s, sig, rw, s->K);
+    if (sweep_inverse(n, s->K)) bad = 1;
+    double xt[MAXNV], zt[MAXR], rhs[MAXNV], tmp[MAXR], Ax[MAXR], Px[MAXNV], Aty[MAXNV];
+    for (int it = 1; it <= p->max_iter && !bad; ++it) {
+      for (int r = 0; r < m; ++r) tmp[r] = rho * z[r] - y[r];
+      CTmul(s, tmp, rhs);
+      for (int i = 0; i < n; ++i) rhs[i] += sig * x[i] - s->q[i];
+      matvec(n, s->K, rhs, xt);
+      Cmul(s, xt, zt);
+      for (int i = 0; i < n; ++i) x[i] = a * xt[i] + (1.0 - a) * x[i];
+      const double ir = 1.0 / rho;
+      for (int r = 0; r < m; ++r) {
+        const double v = a * zt[r] + (1.0 - a) * z[r];
+        const double vv = v + y[r] * ir;
+        double zn = vv;
+        if (vv > s->u[r])
+          zn = (rho * vv + 2.0 * s->w[r] * s->u[r]) / (rho + 2.0 * s->w[r]);
+        else if (vv < s->l[r])
+          zn = (rho * vv + 2.0 * s->w[r] * s->l[r]) / (rho + 2.0 * s->w[r]);
+        y[r] = y[r] + rho * (v - zn);
+        z[r] = zn;
+      }
+      admm_it = it;
+      if (it % p->check_termination == 0 || it == p->max_iter) {
+        Cmul(s, x, Ax);
+        matvec(n, s->P, x, Px);
+        CTmul(s, y, Aty);
+        double pr = 0, du = 0, nAx = 0, nz = 0, nPx = 0, nAty = 0, nq = 0;
+        double spr = 0, sdu = 0, snAx = 0, snz = 0, snPx = 0, snAty = 0, snq = 0;
+        for (int r = 0; r < m; ++r) {
+          const double ie = 1.0 / s->E[r];
+          pr = fmax(pr, fabs((Ax[r] - z[r]) * ie));
+          nAx = fmax(nAx, fabs(Ax[r] * ie));
+          nz = fmax(nz, fabs(z[r] * ie));
+          spr = fmax(spr, fabs(Ax[r] - z[r]));
+          snAx = fmax(snAx, fabs(Ax[r]));
+          snz = fmax(snz, fabs(z[r]));
+        }
+        for (int i = 0; i < n; ++i) {
+          const double id = 1.0 / s->D[i];
+          const double rd = Px[i] + s->q[i] + Aty[i];
+          du = fmax(du, fabs(rd * id));
+          nPx = fmax(nPx, fabs(Px[i] * id));
+          nAty = fmax(nAty, fabs(Aty[i] * id));
+          nq = fmax(nq, fabs(s->q[i] * id));
+          sdu = fmax(sdu, fabs(rd));
+          snPx = fmax(snPx, fabs(Px[i]));
+          snAty = fmax(snAty, fabs(Aty[i]));
+          snq = fmax(snq, fabs(s->q[i]));
+        }
+        const double ic = 1.0 / s->c;
+        du *= ic;
+        const double ep = p->eps_abs + p->eps_rel * fmax(nAx, nz);
+        const double ed = p->eps_abs + p->eps_rel * fmax(fmax(nPx, nAty), nq) * ic;
+        if (!isfinite(pr) || !isfinite(du)) {
+          bad = 1;
+          break;
+        }
+        if (pr <= ep && du <= ed) {
+          admm_ok = 1;
+          break;
+        }
+        if (p->adaptive_rho && it % p->adaptive_rho_interval == 0) {
+          const double pn = spr / (fmax(snAx, snz) + DIV_TOL);
+          const double dn = sdu / (fmax(fmax(snPx, snAty), snq) + DIV_TOL);
+          double rn = rho * sqrt(pn / (dn + DIV_TOL));
+          rn = fmin(fmax(rn, RHO_MIN), RHO_MAX);
+          if (rn > rho * p->adaptive_rho_tolerance || rn < rho / p->adaptive_rho_tolerance) {
+            rho = rn;
+            for (int r = 0; r < m; ++r) rw[r] = rho;
+            form_kkt(s, sig, rw, s->K);
+            if (sweep_inverse(n, s->K)) bad = 1;
+          }
+        }
+      }
+    }
+    st = admm_ok ? MPCQP_SOLVED : MPCQP_MAX_ITER_REACHED;
+  }
+
+  /* ---- polish: semismooth Newton / active-set iteration on the scaled problem ---- */
+  const int do_polish = (p->method == MPCQP_METHOD_NEWTON) || p->polish;
+  double xa[MAXNV];
+  memcpy(xa, x, sizeof(double) * n);
+  if (do_polish && !bad) {
+    int pol_ok = 0;
+    uint8_t cd[MAXR], cn[MAXR];
+    double zc[MAXR], rw[MAXR], tmp[MAXR], rhs[MAXNV], xn[MAXNV], res[MAXNV], dx[MAXNV], Px[MAXNV], Pd[MAXNV],
+        zd[MAXR], gr[MAXNV];
+    Cmul(s, x, zc);
+    codes_of(s, zc, cd);
+    for (int it = 1; it <= p->polish_max_iter; ++it) {
+      pol_it = it;
+      for (int r = 0; r < m; ++r) {
+        rw[r] = cd[r] ? 2.0 * s->w[r] : 0.0;
+        tmp[r] = cd[r] == 2 ? rw[r] * s->u[r] : (cd[r] == 1 ? rw[r] * s->l[r] : 0.0);
+      }
+      form_kkt(s, 0.0, rw, s->M);
+      memcpy(s->K, s->M, sizeof(s->M));
+      if (sweep_inverse(n, s->K)) {
+        bad = 1;
+        break;
+      }
+      CTmul(s, tmp, rhs);
+      for (int i = 0; i < n; ++i) rhs[i] -= s->q[i];
+      matvec(n, s->K, rhs, xn);
+      /* one step of iterative refinement */
+      matvec(n, s->M, xn, res);
+      for (int i = 0; i < n; ++i) res[i] = rhs[i] - res[i];
+      matvec(n, s->K, res, dx);
+      for (int i = 0; i < n; ++i) xn[i] += dx[i];
+      double zn[MAXR];
+      Cmul(s, xn, zn);
+      codes_of(s, zn, cn);
+      if (memcmp(cn, cd, m) == 0) {
+        memcpy(x, xn, sizeof(double) * n);
+        pol_ok = 1;
+        break;
+      }
+      /* Armijo backtracking on the scaled objective along d = xn - x */
+      for (int i = 0; i < n; ++i) dx[i] = xn[i] - x[i];
+      matvec(n, s->P, x, Px);
+      matvec(n, s->P, dx, Pd);
+      for (int r = 0; r < m; ++r) {
+        zd[r] = zn[r] - zc[r];
+        const double rr = zc[r] > s->u[r] ? zc[r] - s->u[r] : (zc[r] < s->l[r] ? zc[r] - s->l[r] : 0.0);
+        tmp[r] = 2.0 * s->w[r] * rr;
+      }
+      CTmul(s, tmp, gr);
+      double slope = 0.0, qd = 0.0, lin = 0.0, q0 = 0.0;
+      for (int i = 0; i < n; ++i) {
+        slope += (Px[i] + s->q[i] + gr[i]) * dx[i];
+        qd += dx[i] * Pd[i];
+        lin += (Px[i] + s->q[i]) * dx[i];
+        q0 += x[i] * (0.5 * Px[i] + s->q[i]);
+      }
+      const double f0 = q0 + pen(s, zc);
+      double t = 1.0;
+      for (int ls = 0; ls < 60; ++ls) {
+        double zt[MAXR];
+        for (int r = 0; r < m; ++r) zt[r] = zc[r] + t * zd[r];
+        const double ft = q0 + t * lin + 0.5 * t * t * qd + pen(s, zt);
+        if (ft <= f0 + 1e-4 * t * slope) break;
+        t *= 0.5;
+      }
+      for (int i = 0; i < n; ++i) x[i] += t * dx[i];
+      for (int r = 0; r < m; ++r) zc[r] = zc[r] + t * zd[r];
+      Cmul(s, x, zc);
+      codes_of(s, zc, cd);
+    }
+    if (pol_ok)
+      st = MPCQP_SOLVED;
+    else if (p->method == MPCQP_METHOD_ADMM) {
+      memcpy(x, xa, sizeof(double) * n);
+      st = admm_ok ? MPCQP_SOLVED_INACCURATE : MPCQP_MAX_ITER_REACHED;
+    } else
+      st = MPCQP_MAX_ITER_REACHED;
+  }
+  if (bad) st = MPCQP_NUMERICAL_ERROR;
+
+  /* ---- outputs (unscaled) ---- */
+  double U[MAXNV];
+  for (int i = 0; i < n; ++i) U[i] = s->D[i] * x[i];
+  double X[4][MAXN + 1];
+  X[0][0] = x0[0];
+  X[1][0] = x0[1];
+  X[2][0] = x0[2];
+  X[3][0] = x0[3];
+  for (int k = 0; k < N; ++k) {
+    const double psi = X[2][k], v = X[3][k];
+    X[0][k + 1] = X[0][k] + al[k] * psi + be[k] * v + c0[k];
+    X[1][k + 1] = X[1][k] + ga[k] * psi + et[k] * v + c1[k];
+    X[2][k + 1] = psi + si[k] * U[2 * k + 1];
+    X[3][k + 1] = v + p->dt * U[2 * k];
+  }
+  if (u0) {
+    u0[0] = U[0];
+    u0[1] = U[1];
+  }
+  if (Uo)
+    for (int k = 0; k < N; ++k) {
+      Uo[k] = U[2 * k];
+      Uo[N + k] = U[2 * k + 1];
+    }
+  if (Xo)
+    for (int c = 0; c < 4; ++c)
+      for (int k = 0; k <= N; ++k) Xo[c * (N + 1) + k] = X[c][k];
+  if (active) {
+    for (int k = 0; k <= N; ++k) {
+      const double v = X[3][k];
+      active[k] = v > p->v_bounds[1] ? 2 : (v < p->v_bounds[0] ? 1 : 0);
+    }
+    for (int q = 0; q < n; ++q) {
+      const int c = q & 1;
+      const double uu = U[q];
+      active[N + 1 + q] = uu > p->u_bounds[2 * c + 1] ? 2 : (uu < p->u_bounds[2 * c] ? 1 : 0);
+      const double d = uu - (q < 2 ? up[c] : U[q - 2]);
+      active[3 * N + 1 + q] = d > p->du_bounds[2 * c + 1] ? 2 : (d < p->du_bounds[2 * c] ? 1 : 0);
+    }
+  }
+  if (status) *status = st;
+  if (iters) {
+    iters[0] = admm_it;
+    iters[1] = pol_it;
+  }
+}
+
+/* Same contract as mpcqp_build + mpcqp_solve on HOST pointers, OpenMP over the batch. */
+int mpcqp_cpu_solve(const mpcqp_params* p, int B, const double* x0, const double* ref, const double* u_prev,
+                    double* u0, double* X, double* U, int32_t* status, int32_t* iters, uint8_t* active,
+                    double* model_out, int nthreads) {
+  if (!p || B < 0 || !x0 || !ref) return MPCQP_E_ARG;
+  const int N = p->horizon;
+  if (N < 1 || N > MAXN) return MPCQP_E_HORIZON;
+  const int S = mpcqp_model_stride(N);
+#ifdef _OPENMP
+  if (nthreads > 0) omp_set_num_threads(nthreads);
+#pragma omp parallel for schedule(dynamic, 4)
+#endif
+  for (int b = 0; b < B; ++b) {
+    double model[16 * MAXN + 16];
+    mpcqp_cpu_build_one(p, x0 + 4 * (size_t)b, ref + 4 * (size_t)(N + 1) * b, u_prev ? u_prev + 2 * (size_t)b : NULL,
+                        model);
+    if (model_out) memcpy(model_out + (size_t)S * b, model, sizeof(double) * S);
+    mpcqp_cpu_solve_one(p, model, u0 ? u0 + 2 * (size_t)b : NULL, X ? X + 4 * (size_t)(N + 1) * b : NULL,
+                        U ? U + 2 * (size_t)N * b : NULL, status ? status + b : NULL, iters ? iters + 2 * (size_t)b : NULL,
+                        active ? active + (size_t)(5 * N + 1) * b : NULL);
+  }
+  return MPCQP_OK;
+}
