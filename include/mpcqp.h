@@ -137,7 +137,8 @@ int mpcqp_build(mpcqp_ws* ws, int B, const double* x0, const double* ref, const 
  *   X      B x 4 x (N+1)     predicted states, X[:,0] = x0
  *   U      B x 2 x N         inputs
  *   status B                 MPCQP_SOLVED / ... per QP
- *   iters  B x 2             {ADMM iterations, polish iterations}
+ *   iters  B x 4             {ADMM iterations, polish iterations, KKT factorizations,
+ *                             line-search trials}
  *   active B x (5N+1)        MPCQP_ROW_* per soft row at the returned solution
  */
 int mpcqp_solve(mpcqp_ws* ws, int B, double* u0, double* X, double* U, int32_t* status,

@@ -121,7 +121,7 @@ def cpu_solve(params, x0, ref, u_prev=None, *, method: int = 0, nthreads: int = 
         X=np.zeros((B, 4, N + 1)),
         U=np.zeros((B, 2, N)),
         status=np.zeros(B, np.int32),
-        iters=np.zeros((B, 2), np.int32),
+        iters=np.zeros((B, 4), np.int32),
         active=np.zeros((B, 5 * N + 1), np.uint8),
     )
     model = np.zeros((B, L.mpcqp_model_stride(N))) if want_model else None

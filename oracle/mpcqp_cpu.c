@@ -359,7 +359,7 @@ void mpcqp_cpu_solve_one(const mpcqp_params* p, const double* model, double* u0,
   const double* x0 = model + 11 * N + 4;
   const double* up = model + 11 * N + 8;
   int st = MPCQP_MAX_ITER_REACHED;
-  int admm_it = 0, pol_it = 0;
+  int admm_it = 0, pol_it = 0, n_fact = 0, n_ls = 0;
 
   condense(p, model, s);
   /* unscaled problem data: P = 2H, q = 2g, bounds with the row offsets folded in */
@@ -449,6 +449,7 @@ void mpcqp_cpu_solve_one(const mpcqp_params* p, const double* model, double* u0,
     double rw[MAXR];
     for (int r = 0; r < m; ++r) rw[r] = rho;
     form_kkt(s, sig, rw, s->K);
+    ++n_fact;
     if (sweep_inverse(n, s->K)) bad = 1;
     double xt[MAXNV], zt[MAXR], rhs[MAXNV], tmp[MAXR], Ax[MAXR], Px[MAXNV], Aty[MAXNV];
     for (int it = 1; it <= p->max_iter && !bad; ++it) {
@@ -519,6 +520,7 @@ void mpcqp_cpu_solve_one(const mpcqp_params* p, const double* model, double* u0,
             rho = rn;
             for (int r = 0; r < m; ++r) rw[r] = rho;
             form_kkt(s, sig, rw, s->K);
+            ++n_fact;
             if (sweep_inverse(n, s->K)) bad = 1;
           }
         }
@@ -545,6 +547,7 @@ void mpcqp_cpu_solve_one(const mpcqp_params* p, const double* model, double* u0,
         tmp[r] = cd[r] == 2 ? rw[r] * s->u[r] : (cd[r] == 1 ? rw[r] * s->l[r] : 0.0);
       }
       form_kkt(s, 0.0, rw, s->M);
+      ++n_fact;
       memcpy(s->K, s->M, sizeof(s->M));
       if (sweep_inverse(n, s->K)) {
         bad = 1;
@@ -586,6 +589,7 @@ void mpcqp_cpu_solve_one(const mpcqp_params* p, const double* model, double* u0,
       const double f0 = q0 + pen(s, zc);
       double t = 1.0;
       for (int ls = 0; ls < 60; ++ls) {
+        ++n_ls;
         double zt[MAXR];
         for (int r = 0; r < m; ++r) zt[r] = zc[r] + t * zd[r];
         const double ft = q0 + t * lin + 0.5 * t * t * qd + pen(s, zt);
@@ -651,6 +655,8 @@ void mpcqp_cpu_solve_one(const mpcqp_params* p, const double* model, double* u0,
   if (iters) {
     iters[0] = admm_it;
     iters[1] = pol_it;
+    iters[2] = n_fact;
+    iters[3] = n_ls;
   }
 }
 
@@ -672,7 +678,7 @@ int mpcqp_cpu_solve(const mpcqp_params* p, int B, const double* x0, const double
                         model);
     if (model_out) memcpy(model_out + (size_t)S * b, model, sizeof(double) * S);
     mpcqp_cpu_solve_one(p, model, u0 ? u0 + 2 * (size_t)b : NULL, X ? X + 4 * (size_t)(N + 1) * b : NULL,
-                        U ? U + 2 * (size_t)N * b : NULL, status ? status + b : NULL, iters ? iters + 2 * (size_t)b : NULL,
+                        U ? U + 2 * (size_t)N * b : NULL, status ? status + b : NULL, iters ? iters + 4 * (size_t)b : NULL,
                         active ? active + (size_t)(5 * N + 1) * b : NULL);
   }
   return MPCQP_OK;

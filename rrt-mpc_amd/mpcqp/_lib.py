@@ -1,0 +1,179 @@
+"""ctypes binding of ``libmpcqp.so`` (the C-ABI of ``include/mpcqp.h``).
+
+The shared library is built in-tree by ``__graft_entry__.build()`` (hipcc,
+``--offload-arch=gfx950``) next to this file.  There is no fallback: if the
+library is missing or fails to load, every solver entry point raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from pathlib import Path
+from typing import Optional
+
+import numpy as np
+
+LIB_NAME = "libmpcqp.so"
+LIB_PATH = Path(os.environ.get("MPCQP_LIB", Path(__file__).resolve().parent / LIB_NAME))
+
+# constants mirrored from include/mpcqp.h
+MAX_HORIZON = 31
+SOLVED = 1
+SOLVED_INACCURATE = 2
+MAX_ITER_REACHED = -2
+NUMERICAL_ERROR = -10
+METHOD_ADMM = 0
+METHOD_NEWTON = 1
+STATUS_NAMES = {
+    SOLVED: "solved",
+    SOLVED_INACCURATE: "solved_inaccurate",
+    MAX_ITER_REACHED: "maximum_iterations_reached",
+    NUMERICAL_ERROR: "numerical_error",
+}
+
+# OSQP settings used by the reference (src/control/mpc_controller.py:121-131) plus the
+# OSQP defaults it relies on implicitly.
+DEFAULT_SOLVER_SETTINGS = dict(
+    rho=0.1,
+    sigma=1e-6,
+    alpha=1.6,
+    eps_abs=1e-3,
+    eps_rel=1e-3,
+    adaptive_rho_tolerance=5.0,
+    max_iter=60000,
+    check_termination=25,
+    scaling=10,
+    adaptive_rho=1,
+    adaptive_rho_interval=25,
+    polish=1,
+    polish_max_iter=100,
+)
+
+
+class MpcqpParams(ctypes.Structure):
+    """``mpcqp_params`` (include/mpcqp.h)."""
+
+    _fields_ = [
+        ("horizon", ctypes.c_int32),
+        ("method", ctypes.c_int32),
+        ("wheelbase_px", ctypes.c_double),
+        ("dt", ctypes.c_double),
+        ("q", ctypes.c_double * 16),
+        ("r", ctypes.c_double * 4),
+        ("q_terminal", ctypes.c_double * 16),
+        ("u_bounds", ctypes.c_double * 4),
+        ("v_bounds", ctypes.c_double * 2),
+        ("du_bounds", ctypes.c_double * 4),
+        ("slack_velocity", ctypes.c_double),
+        ("slack_input", ctypes.c_double),
+        ("slack_rate", ctypes.c_double),
+        ("rho", ctypes.c_double),
+        ("sigma", ctypes.c_double),
+        ("alpha", ctypes.c_double),
+        ("eps_abs", ctypes.c_double),
+        ("eps_rel", ctypes.c_double),
+        ("adaptive_rho_tolerance", ctypes.c_double),
+        ("max_iter", ctypes.c_int32),
+        ("check_termination", ctypes.c_int32),
+        ("scaling", ctypes.c_int32),
+        ("adaptive_rho", ctypes.c_int32),
+        ("adaptive_rho_interval", ctypes.c_int32),
+        ("polish", ctypes.c_int32),
+        ("polish_max_iter", ctypes.c_int32),
+        ("reserved", ctypes.c_int32),
+    ]
+
+
+def to_c_params(params, method: int = METHOD_ADMM, **settings) -> MpcqpParams:
+    """Fill ``mpcqp_params`` from an ``MPCParameters``-like object (mpc_controller.py:17-30)."""
+    c = MpcqpParams()
+    c.horizon = int(params.horizon)
+    c.method = int(method)
+    c.wheelbase_px = float(params.wheelbase_px)
+    c.dt = float(params.dt)
+    c.q[:] = [float(v) for v in np.asarray(params.q, dtype=float).reshape(16)]
+    c.r[:] = [float(v) for v in np.asarray(params.r, dtype=float).reshape(4)]
+    c.q_terminal[:] = [float(v) for v in np.asarray(params.q_terminal, dtype=float).reshape(16)]
+    c.u_bounds[:] = [float(v) for v in np.asarray(params.u_bounds, dtype=float).reshape(4)]
+    c.v_bounds[:] = [float(v) for v in np.asarray(params.v_bounds, dtype=float).reshape(2)]
+    c.du_bounds[:] = [float(v) for v in np.asarray(params.du_bounds, dtype=float).reshape(4)]
+    c.slack_velocity = float(getattr(params, "slack_velocity", 1e3))
+    c.slack_input = float(getattr(params, "slack_input", 5e2))
+    c.slack_rate = float(getattr(params, "slack_rate", 5e2))
+    merged = dict(DEFAULT_SOLVER_SETTINGS)
+    merged.update(settings)
+    for key, value in merged.items():
+        setattr(c, key, value)
+    return c
+
+
+class LibraryError(RuntimeError):
+    pass
+
+
+_lib: Optional[ctypes.CDLL] = None
+
+_SYMBOLS = {
+    "mpcqp_version": ([], ctypes.c_int),
+    "mpcqp_last_error": ([], ctypes.c_char_p),
+    "mpcqp_num_rows": ([ctypes.c_int], ctypes.c_int),
+    "mpcqp_create": ([ctypes.POINTER(MpcqpParams), ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_void_p)],
+                     ctypes.c_int),
+    "mpcqp_set_params": ([ctypes.c_void_p, ctypes.POINTER(MpcqpParams)], ctypes.c_int),
+    "mpcqp_destroy": ([ctypes.c_void_p], None),
+    "mpcqp_build": ([ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                     ctypes.c_void_p], ctypes.c_int),
+    "mpcqp_solve": ([ctypes.c_void_p, ctypes.c_int] + [ctypes.c_void_p] * 7, ctypes.c_int),
+    "mpcqp_model_buffer": ([ctypes.c_void_p], ctypes.c_void_p),
+    "mpcqp_model_stride": ([ctypes.c_int], ctypes.c_int),
+}
+
+
+def exported_symbols():
+    return list(_SYMBOLS)
+
+
+def lib() -> ctypes.CDLL:
+    """Load ``libmpcqp.so``; raises ``LibraryError`` (no fallback) when it is absent."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not LIB_PATH.exists():
+        raise LibraryError(
+            f"{LIB_PATH} not found: build it with `python -c 'import __graft_entry__ as g; g.build()'` "
+            "(hipcc --offload-arch=gfx950).  The MPC solver has no CPU fallback."
+        )
+    handle = ctypes.CDLL(str(LIB_PATH))
+    for name, (argtypes, restype) in _SYMBOLS.items():
+        fn = getattr(handle, name)
+        fn.argtypes = argtypes
+        fn.restype = restype
+    if handle.mpcqp_version() != 1:
+        raise LibraryError("libmpcqp ABI version mismatch")
+    _lib = handle
+    return handle
+
+
+def check(rc: int, what: str) -> None:
+    if rc != 0:
+        msg = lib().mpcqp_last_error().decode(errors="replace")
+        raise LibraryError(f"{what} failed ({rc}): {msg}")
+
+
+__all__ = [
+    "MpcqpParams",
+    "to_c_params",
+    "lib",
+    "check",
+    "LibraryError",
+    "DEFAULT_SOLVER_SETTINGS",
+    "STATUS_NAMES",
+    "SOLVED",
+    "SOLVED_INACCURATE",
+    "MAX_ITER_REACHED",
+    "NUMERICAL_ERROR",
+    "METHOD_ADMM",
+    "METHOD_NEWTON",
+    "MAX_HORIZON",
+    "exported_symbols",
+]

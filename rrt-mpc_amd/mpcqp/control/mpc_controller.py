@@ -1,0 +1,227 @@
+"""Linear time-varying MPC on MI355X: drop-in for ``src/control/mpc_controller.py``.
+
+``MPCParameters`` and ``MPCController.solve`` keep the reference's names,
+arguments, return values and failure behaviour (``mpc_controller.py:17-145``);
+the QP that the reference assembles in cvxpy and hands to OSQP
+(``:53-132``) is built and solved by the HIP kernels of ``libmpcqp.so``
+(``csrc/mpcqp.hip``: K1 ``k_build`` = unwrap + linearize, K2 ``k_solve`` =
+condense + OSQP-algorithm ADMM + polish).  ``BatchedMPCController`` is the
+batched entry point that thousands of candidate trajectories go through at once.
+"""
+from __future__ import annotations
+
+import ctypes
+import logging
+from collections import OrderedDict
+from dataclasses import dataclass
+from typing import NamedTuple, Optional, Tuple
+
+import numpy as np
+
+from .. import _lib
+
+LOG = logging.getLogger(__name__)
+
+FloatArray = np.ndarray
+
+
+@dataclass
+class MPCParameters:
+    """Same fields and defaults as ``src/control/mpc_controller.py:17-30``."""
+
+    wheelbase_px: float
+    dt: float
+    horizon: int
+    q: FloatArray
+    r: FloatArray
+    q_terminal: FloatArray
+    u_bounds: Tuple[Tuple[float, float], Tuple[float, float]]
+    v_bounds: Tuple[float, float]
+    du_bounds: Tuple[Tuple[float, float], Tuple[float, float]]
+    slack_velocity: float = 1e3
+    slack_input: float = 5e2
+    slack_rate: float = 5e2
+
+
+class BatchSolution(NamedTuple):
+    """Device tensors of one ``solve_batch`` call (views into controller-owned buffers,
+    valid until the next call on the same controller)."""
+
+    u0: "object"  # (B, 2)      float64
+    X: "object"  # (B, 4, N+1)  float64
+    U: "object"  # (B, 2, N)    float64
+    status: "object"  # (B,)    int32   (1 solved, 2 solved_inaccurate, -2 max_iter, -10 numerical)
+    iters: "object"  # (B, 4)   int32   {ADMM its, polish its, KKT factorizations, line-search trials}
+    active: "object"  # (B, 5N+1) uint8 {0 inactive, 1 lower, 2 upper} per soft row
+
+
+def _params_key(params, method: int, settings: dict) -> tuple:
+    return (
+        int(params.horizon),
+        float(params.wheelbase_px),
+        float(params.dt),
+        np.asarray(params.q, float).tobytes(),
+        np.asarray(params.r, float).tobytes(),
+        np.asarray(params.q_terminal, float).tobytes(),
+        np.asarray(params.u_bounds, float).tobytes(),
+        np.asarray(params.v_bounds, float).tobytes(),
+        np.asarray(params.du_bounds, float).tobytes(),
+        float(getattr(params, "slack_velocity", 1e3)),
+        float(getattr(params, "slack_input", 5e2)),
+        float(getattr(params, "slack_rate", 5e2)),
+        int(method),
+        tuple(sorted(settings.items())),
+    )
+
+
+class BatchedMPCController:
+    """Solve B independent MPC QPs per call on one GPU.
+
+    ``solve_batch(x0[B,4], ref[B,N+1,4], u_prev[B,2])`` runs K1 + K2 asynchronously on
+    the current torch stream (or ``stream``).  Inputs may be numpy arrays (copied to the
+    device) or float64 device tensors (used in place).
+    """
+
+    def __init__(self, params, max_batch: int, *, device=None, method: str = "admm", **settings) -> None:
+        import torch
+
+        if method not in ("admm", "newton"):
+            raise ValueError("method must be 'admm' or 'newton'")
+        if not torch.cuda.is_available():
+            raise _lib.LibraryError("BatchedMPCController needs a ROCm GPU; there is no CPU fallback")
+        self._torch = torch
+        self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+        if self.device.index is None:
+            self.device = torch.device("cuda", torch.cuda.current_device())
+        self.params = params
+        self.method = _lib.METHOD_ADMM if method == "admm" else _lib.METHOD_NEWTON
+        self.settings = dict(settings)
+        self.horizon = int(params.horizon)
+        self.max_batch = int(max_batch)
+        L = _lib.lib()
+        self._L = L
+        self._cparams = _lib.to_c_params(params, self.method, **self.settings)
+        ws = ctypes.c_void_p()
+        with torch.cuda.device(self.device):
+            _lib.check(L.mpcqp_create(ctypes.byref(self._cparams), self.max_batch, self.device.index, ctypes.byref(ws)),
+                       "mpcqp_create")
+        self._ws = ws
+        N, B = self.horizon, self.max_batch
+        kw = dict(device=self.device)
+        self._u0 = torch.empty((B, 2), dtype=torch.float64, **kw)
+        self._X = torch.empty((B, 4, N + 1), dtype=torch.float64, **kw)
+        self._U = torch.empty((B, 2, N), dtype=torch.float64, **kw)
+        self._status = torch.empty((B,), dtype=torch.int32, **kw)
+        self._iters = torch.empty((B, 4), dtype=torch.int32, **kw)
+        self._active = torch.empty((B, 5 * N + 1), dtype=torch.uint8, **kw)
+
+    # ------------------------------------------------------------------
+    def set_params(self, params) -> None:
+        """Swap the parameter block (same horizon); stream-ordered."""
+        self._cparams = _lib.to_c_params(params, self.method, **self.settings)
+        _lib.check(self._L.mpcqp_set_params(self._ws, ctypes.byref(self._cparams)), "mpcqp_set_params")
+        self.params = params
+
+    def _device_input(self, a, shape, name):
+        torch = self._torch
+        if isinstance(a, torch.Tensor):
+            t = a
+            if t.device != self.device or t.dtype != torch.float64:
+                t = t.to(device=self.device, dtype=torch.float64)
+        else:
+            t = torch.from_numpy(np.ascontiguousarray(a, dtype=np.float64)).to(self.device, non_blocking=False)
+        t = t.contiguous()
+        if tuple(t.shape) != tuple(shape):
+            t = t.reshape(shape)
+        return t
+
+    def solve_batch(self, x0, ref, u_prev=None, *, stream=None) -> BatchSolution:
+        torch = self._torch
+        N = self.horizon
+        B = int(x0.shape[0])
+        if B > self.max_batch:
+            raise ValueError(f"batch {B} exceeds max_batch {self.max_batch}")
+        x0_t = self._device_input(x0, (B, 4), "x0")
+        ref_t = self._device_input(ref, (B, N + 1, 4), "ref")
+        up_t = None if u_prev is None else self._device_input(u_prev, (B, 2), "u_prev")
+        if stream is None:
+            stream = torch.cuda.current_stream(self.device)
+        s = ctypes.c_void_p(stream.cuda_stream)
+        self._keep = (x0_t, ref_t, up_t)  # keep inputs alive until the kernels have consumed them
+        _lib.check(self._L.mpcqp_build(self._ws, B, x0_t.data_ptr(), ref_t.data_ptr(),
+                                       None if up_t is None else up_t.data_ptr(), s), "mpcqp_build")
+        _lib.check(self._L.mpcqp_solve(self._ws, B, self._u0.data_ptr(), self._X.data_ptr(), self._U.data_ptr(),
+                                       self._status.data_ptr(), self._iters.data_ptr(), self._active.data_ptr(), s),
+                   "mpcqp_solve")
+        return BatchSolution(self._u0[:B], self._X[:B], self._U[:B], self._status[:B], self._iters[:B],
+                             self._active[:B])
+
+    def close(self) -> None:
+        if getattr(self, "_ws", None) is not None and self._ws.value:
+            self._L.mpcqp_destroy(self._ws)
+            self._ws = ctypes.c_void_p()
+
+    def __del__(self):  # pragma: no cover - interpreter shutdown order
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+_CACHE: "OrderedDict[tuple, BatchedMPCController]" = OrderedDict()
+_CACHE_SIZE = 8
+
+
+def _single_controller(params, method: str = "admm", **settings) -> BatchedMPCController:
+    key = _params_key(params, 0 if method == "admm" else 1, settings)
+    ctrl = _CACHE.get(key)
+    if ctrl is None:
+        ctrl = BatchedMPCController(params, 1, method=method, **settings)
+        _CACHE[key] = ctrl
+        while len(_CACHE) > _CACHE_SIZE:
+            _CACHE.popitem(last=False)[1].close()
+    else:
+        _CACHE.move_to_end(key)
+    return ctrl
+
+
+class MPCController:
+    """Quadratic-cost MPC controller with soft bounds and rate limits (``mpc_controller.py:33-145``)."""
+
+    def __init__(self, params: MPCParameters) -> None:
+        self._params = params
+
+    def solve(
+        self,
+        x0: FloatArray,
+        ref_traj: FloatArray,
+        *,
+        u_init: Optional[FloatArray] = None,
+        u_prev: Optional[FloatArray] = None,
+    ) -> Tuple[Optional[FloatArray], Optional[FloatArray], Optional[FloatArray]]:
+        # u_init is accepted and ignored, as in the reference (mpc_controller.py:50-51).
+        N = int(self._params.horizon)
+        x0 = np.asarray(x0, dtype=float).reshape(1, 4)
+        ref = np.asarray(ref_traj, dtype=float)
+        if ref.shape != (N + 1, 4):
+            raise ValueError(f"ref_traj must have shape {(N + 1, 4)}, got {ref.shape}")
+        up = np.zeros((1, 2)) if u_prev is None else np.asarray(u_prev, dtype=float).reshape(1, 2)
+        ctrl = _single_controller(self._params)
+        sol = ctrl.solve_batch(x0, ref[None], up)
+        status = int(sol.status.cpu()[0])
+        if status == _lib.NUMERICAL_ERROR:
+            LOG.error("MPC solve failed with a numerical error")
+            return None, None, None
+        if status not in (_lib.SOLVED, _lib.SOLVED_INACCURATE):
+            LOG.warning("MPC solve returned status %s", _lib.STATUS_NAMES.get(status, status))
+            return None, None, None
+        U = sol.U[0].cpu().numpy().copy()
+        X = sol.X[0].cpu().numpy().copy()
+        return U[:, 0].copy(), X, U
+
+    @property
+    def params(self) -> MPCParameters:
+        return self._params
+
+
+__all__ = ["MPCParameters", "MPCController", "BatchedMPCController", "BatchSolution"]
