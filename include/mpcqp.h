@@ -144,10 +144,17 @@ int mpcqp_build(mpcqp_ws* ws, int B, const double* x0, const double* ref, const 
 int mpcqp_solve(mpcqp_ws* ws, int B, double* u0, double* X, double* U, int32_t* status,
                 int32_t* iters, uint8_t* active, void* stream);
 
-/* Workspace device buffer holding the K1 output (for tests / inspection):
- * B x mpcqp_model_stride(N) doubles, layout documented in DESIGN.md. */
+/* Workspace device buffers (for tests / inspection), layouts documented in DESIGN.md:
+ *   model: K1 output, B x mpcqp_model_stride(N) doubles
+ *   state: scaled QP + ADMM iterate (K2a/K2b output), B x mpcqp_state_stride(N) doubles */
 const double* mpcqp_model_buffer(const mpcqp_ws* ws);
 int mpcqp_model_stride(int horizon);
+const double* mpcqp_state_buffer(const mpcqp_ws* ws);
+int mpcqp_state_stride(int horizon);
+
+/* Test hook: applies the kernels' 64-lane wavefront primitives (DPP prefix/suffix scans,
+ * reductions, lane shifts) to in[64] -> out[10 x 64] on the device. */
+int mpcqp_debug_wave_ops(const double* in, double* out, void* stream);
 
 #ifdef __cplusplus
 }

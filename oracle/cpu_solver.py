@@ -138,4 +138,20 @@ def cpu_solve(params, x0, ref, u_prev=None, *, method: int = 0, nthreads: int = 
     return out
 
 
-__all__ = ["CParams", "make_cparams", "cpu_solve", "build_library", "lib"]
+def cpu_state(params, model: np.ndarray, state_stride: int, **solver) -> np.ndarray:
+    """Scaled QP (GPU state layout) for each model row: (B, state_stride)."""
+    L = lib()
+    if not hasattr(L, "_state_bound"):
+        L.mpcqp_cpu_state.argtypes = [ctypes.POINTER(CParams), ctypes.POINTER(ctypes.c_double),
+                                      ctypes.POINTER(ctypes.c_double)]
+        L.mpcqp_cpu_state.restype = None
+        L._state_bound = True
+    cp = make_cparams(params, 0, **solver)
+    model = np.ascontiguousarray(model, dtype=np.float64)
+    out = np.zeros((model.shape[0], state_stride))
+    for b in range(model.shape[0]):
+        L.mpcqp_cpu_state(ctypes.byref(cp), _p(model[b], ctypes.c_double), _p(out[b], ctypes.c_double))
+    return out
+
+
+__all__ = ["CParams", "make_cparams", "cpu_solve", "cpu_state", "build_library", "lib"]

@@ -339,28 +339,16 @@ static void codes_of(const qp_t* s, const double* z, uint8_t* cd) {
   for (int r = 0; r < s->m; ++r) cd[r] = z[r] > s->u[r] ? 2 : (z[r] < s->l[r] ? 1 : 0);
 }
 
-/* ---------------------------------------------------------------- one QP */
-void mpcqp_cpu_solve_one(const mpcqp_params* p, const double* model, double* u0, double* Xo, double* Uo,
-                         int32_t* status, int32_t* iters, uint8_t* active) {
-  qp_t S;
-  qp_t* s = &S;
+/* ---------------------------------------------------------------- setup (GPU K2a) */
+/* condensing + OSQP scaling: fills P, q, D, E, c and the scaled bounds/weights of s */
+static void setup_qp(const mpcqp_params* p, const double* model, qp_t* s) {
   const int N = p->horizon, n = 2 * N, m = 5 * N;
   s->N = N;
   s->n = n;
   s->m = m;
   s->dt = p->dt;
-  const double* al = model;
-  const double* be = model + N;
-  const double* ga = model + 2 * N;
-  const double* et = model + 3 * N;
-  const double* si = model + 4 * N;
-  const double* c0 = model + 5 * N;
-  const double* c1 = model + 6 * N;
   const double* x0 = model + 11 * N + 4;
   const double* up = model + 11 * N + 8;
-  int st = MPCQP_MAX_ITER_REACHED;
-  int admm_it = 0, pol_it = 0, n_fact = 0, n_ls = 0;
-
   condense(p, model, s);
   /* unscaled problem data: P = 2H, q = 2g, bounds with the row offsets folded in */
   for (int i = 0; i < n; ++i) {
@@ -437,6 +425,54 @@ void mpcqp_cpu_solve_one(const mpcqp_params* p, const double* model, double* u0,
     s->u[r] = s->E[r] * hi0[r];
     s->w[r] = s->c * w0[r] / (s->E[r] * s->E[r]);
   }
+}
+
+/* The scaled problem in the GPU state layout (mpcqp_state_buffer): Pbar n x n, then 15 lane
+ * fields x 64 {q, D, x, E[3], lo[3], hi[3], w[3]} with lane p owning rows {v p/2 (p even),
+ * input p, rate p}, then {cscale}.  Used by tests to check K2a. */
+void mpcqp_cpu_state(const mpcqp_params* p, const double* model, double* out) {
+  static _Thread_local qp_t S;
+  qp_t* s = &S;
+  setup_qp(p, model, s);
+  const int N = p->horizon, n = 2 * N;
+  const int lane_off = (4 * N * N + 7) / 8 * 8;
+  for (int i = 0; i < n; ++i)
+    for (int j = 0; j < n; ++j) out[i * n + j] = s->P[i][j];
+  double* lf = out + lane_off;
+  for (int f = 0; f < 15 * 64; ++f) lf[f] = 0.0;
+  for (int q = 0; q < n; ++q) {
+    lf[0 * 64 + q] = s->q[q];
+    lf[1 * 64 + q] = s->D[q];
+    const int rows[3] = {(q & 1) ? -1 : q / 2, N + q, 3 * N + q};
+    for (int k = 0; k < 3; ++k) {
+      if (rows[k] < 0) continue;
+      lf[(3 + k) * 64 + q] = s->E[rows[k]];
+      lf[(6 + k) * 64 + q] = s->l[rows[k]];
+      lf[(9 + k) * 64 + q] = s->u[rows[k]];
+      lf[(12 + k) * 64 + q] = s->w[rows[k]];
+    }
+  }
+  out[lane_off + 15 * 64] = s->c;
+}
+
+/* ---------------------------------------------------------------- one QP */
+void mpcqp_cpu_solve_one(const mpcqp_params* p, const double* model, double* u0, double* Xo, double* Uo,
+                         int32_t* status, int32_t* iters, uint8_t* active) {
+  static _Thread_local qp_t S;
+  qp_t* s = &S;
+  const int N = p->horizon, n = 2 * N, m = 5 * N;
+  const double* al = model;
+  const double* be = model + N;
+  const double* ga = model + 2 * N;
+  const double* et = model + 3 * N;
+  const double* si = model + 4 * N;
+  const double* c0 = model + 5 * N;
+  const double* c1 = model + 6 * N;
+  const double* x0 = model + 11 * N + 4;
+  const double* up = model + 11 * N + 8;
+  int st = MPCQP_MAX_ITER_REACHED;
+  int admm_it = 0, pol_it = 0, n_fact = 0, n_ls = 0;
+  setup_qp(p, model, s);
 
   double x[MAXNV], z[MAXR], y[MAXR];
   for (int i = 0; i < n; ++i) x[i] = 0.0;

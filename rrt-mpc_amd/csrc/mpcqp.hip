@@ -1,16 +1,18 @@
 // mpcqp.hip -- MI355X (gfx950) batched bicycle-MPC QP solver: kernels + C-ABI.
 //
 // Replaces the reference's per-step MPC solve (CagriCatik/RRT-MPC):
-//   K1 k_build  : window -> LTV model   (src/control/mpc_controller.py:59-70,108,
-//                                        src/control/vehicle_model.py:24-45)
-//   K2 k_solve  : condense + ADMM/OSQP + polish
-//                                       (src/control/mpc_controller.py:53-141; OSQP
-//                                        settings of :121-131)
-// One 64-lane wavefront owns one QP (B QPs -> B single-wave workgroups).  The QP
-// never leaves the CU: LDS holds the scaled Hessian, registers hold one row of the
-// KKT inverse per lane, and every vector of the ADMM iteration is distributed one
-// decision variable per lane.  The algorithm is restated sequentially, operation
-// for operation, in oracle/mpcqp_cpu.c (CPU baseline) -- see DESIGN.md.
+//   K1  k_build  : window -> LTV model      (src/control/mpc_controller.py:59-70,108,
+//                                            src/control/vehicle_model.py:24-45)
+//   K2a k_setup  : condense + Ruiz scaling   (mpc_controller.py:53-117 -> OSQP setup)
+//   K2b k_admm   : OSQP ADMM iterations      (mpc_controller.py:119-132, settings :121-131)
+//   K2c k_finish : polish + outputs/status   (OSQP polish; mpc_controller.py:133-141)
+// One 64-lane wavefront owns one QP (B QPs -> B single-wave workgroups).  Every
+// vector of the iteration is distributed one decision variable per lane; the
+// structured constraint operators are DPP wave scans; the KKT inverse lives one
+// row per lane in registers.  The phases are separate kernels so that each gets
+// its own register budget (occupancy); the per-QP solver state between them
+// (scaled Hessian + scaling vectors, ~20 KB at N=20) stays L2/MALL resident.
+// The algorithm is restated sequentially in oracle/mpcqp_cpu.c -- see DESIGN.md.
 #include <hip/hip_runtime.h>
 
 #include <cmath>
@@ -19,6 +21,7 @@
 #include <cstring>
 #include <new>
 #include <string>
+#include <utility>
 
 #include "../../include/mpcqp.h"
 
@@ -32,54 +35,121 @@ constexpr double kMaxScaling = 1e4;
 constexpr double kRhoMin = 1e-6;
 constexpr double kRhoMax = 1e6;
 constexpr double kDivTol = 1e-30;
+constexpr int kChunk = 8;  // broadcast operands kept in flight per dot-product chunk
 
+// ------------------------------------------------------------------ layouts
 __host__ __device__ constexpr int model_stride(int N) { return ((11 * N + 10) + 7) / 8 * 8; }
 
-// ------------------------------------------------------------------ wave primitives
-__device__ __forceinline__ double wave_max(double v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o, kWave));
-  return v;
+// Solver state per QP (doubles):
+//   [0, n*n)            Pbar, symmetric, row-major
+//   lane fields         kF* x 64 doubles, lane-contiguous
+//   scalars             cscale, admm_ok, admm_it, n_fact
+enum LaneField {
+  kFq = 0,
+  kFD,
+  kFx,
+  kFE0,
+  kFE1,
+  kFE2,
+  kFlo0,
+  kFlo1,
+  kFlo2,
+  kFhi0,
+  kFhi1,
+  kFhi2,
+  kFw0,
+  kFw1,
+  kFw2,
+  kNumFields
+};
+__host__ __device__ constexpr int state_lane_off(int N) { return (4 * N * N + 7) / 8 * 8; }
+__host__ __device__ constexpr int state_scal_off(int N) { return state_lane_off(N) + kNumFields * kWave; }
+__host__ __device__ constexpr int state_stride(int N) { return state_scal_off(N) + 8; }
+
+// ------------------------------------------------------------------ wave primitives (DPP)
+template <int CTRL>
+__device__ __forceinline__ double dpp(double v) {
+  const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), CTRL, 0xf, 0xf, true);
+  const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), CTRL, 0xf, 0xf, true);
+  return __hiloint2double(hi, lo);
 }
-__device__ __forceinline__ double wave_sum(double v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, kWave);
-  return v;
+__device__ __forceinline__ double readlane(double v, int l) {
+  return __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(v), l),
+                          __builtin_amdgcn_readlane(__double2loint(v), l));
 }
-// inclusive prefix sum / max over lanes 0..lane
-__device__ __forceinline__ double scan_sum(double v, int lane) {
-#pragma unroll
-  for (int d = 1; d < kWave; d <<= 1) {
-    double t = __shfl_up(v, d, kWave);
-    if (lane >= d) v += t;
-  }
-  return v;
+constexpr int kRowShr1 = 0x111, kRowShr2 = 0x112, kRowShr4 = 0x114, kRowShr8 = 0x118;
+constexpr int kRowShl1 = 0x101, kRowShl2 = 0x102, kRowShl4 = 0x104, kRowShl8 = 0x108;
+constexpr int kWaveShr1 = 0x138, kWaveShl1 = 0x130;
+
+// inclusive prefix sum over lanes 0..lane (zero-filled row shifts + row totals)
+__device__ __forceinline__ double scan_add(double v, int lane) {
+  v += dpp<kRowShr1>(v);
+  v += dpp<kRowShr2>(v);
+  v += dpp<kRowShr4>(v);
+  v += dpp<kRowShr8>(v);
+  const double t0 = readlane(v, 15), t1 = readlane(v, 31), t2 = readlane(v, 47);
+  const int row = lane >> 4;
+  double off = row >= 1 ? t0 : 0.0;
+  if (row >= 2) off += t1;
+  if (row >= 3) off += t2;
+  return v + off;
 }
+// inclusive suffix sum over lanes lane..63
+__device__ __forceinline__ double rscan_add(double v, int lane) {
+  v += dpp<kRowShl1>(v);
+  v += dpp<kRowShl2>(v);
+  v += dpp<kRowShl4>(v);
+  v += dpp<kRowShl8>(v);
+  const double t1 = readlane(v, 16), t2 = readlane(v, 32), t3 = readlane(v, 48);
+  const int row = lane >> 4;
+  double off = row <= 2 ? t3 : 0.0;
+  if (row <= 1) off += t2;
+  if (row <= 0) off += t1;
+  return v + off;
+}
+// inclusive prefix / suffix max of non-negative values
 __device__ __forceinline__ double scan_max(double v, int lane) {
-#pragma unroll
-  for (int d = 1; d < kWave; d <<= 1) {
-    double t = __shfl_up(v, d, kWave);
-    if (lane >= d) v = fmax(v, t);
-  }
-  return v;
-}
-// inclusive suffix sum / max over lanes lane..63
-__device__ __forceinline__ double rscan_sum(double v, int lane) {
-#pragma unroll
-  for (int d = 1; d < kWave; d <<= 1) {
-    double t = __shfl_down(v, d, kWave);
-    if (lane + d < kWave) v += t;
-  }
-  return v;
+  v = fmax(v, dpp<kRowShr1>(v));
+  v = fmax(v, dpp<kRowShr2>(v));
+  v = fmax(v, dpp<kRowShr4>(v));
+  v = fmax(v, dpp<kRowShr8>(v));
+  const double t0 = readlane(v, 15), t1 = readlane(v, 31), t2 = readlane(v, 47);
+  const int row = lane >> 4;
+  double off = row >= 1 ? t0 : 0.0;
+  if (row >= 2) off = fmax(off, t1);
+  if (row >= 3) off = fmax(off, t2);
+  return fmax(v, off);
 }
 __device__ __forceinline__ double rscan_max(double v, int lane) {
-#pragma unroll
-  for (int d = 1; d < kWave; d <<= 1) {
-    double t = __shfl_down(v, d, kWave);
-    if (lane + d < kWave) v = fmax(v, t);
-  }
-  return v;
+  v = fmax(v, dpp<kRowShl1>(v));
+  v = fmax(v, dpp<kRowShl2>(v));
+  v = fmax(v, dpp<kRowShl4>(v));
+  v = fmax(v, dpp<kRowShl8>(v));
+  const double t1 = readlane(v, 16), t2 = readlane(v, 32), t3 = readlane(v, 48);
+  const int row = lane >> 4;
+  double off = row <= 2 ? t3 : 0.0;
+  if (row <= 1) off = fmax(off, t2);
+  if (row <= 0) off = fmax(off, t1);
+  return fmax(v, off);
 }
+// wave-uniform sum / max (row scans + four row totals)
+__device__ __forceinline__ double wave_sum(double v) {
+  v += dpp<kRowShr1>(v);
+  v += dpp<kRowShr2>(v);
+  v += dpp<kRowShr4>(v);
+  v += dpp<kRowShr8>(v);
+  return (readlane(v, 15) + readlane(v, 31)) + (readlane(v, 47) + readlane(v, 63));
+}
+__device__ __forceinline__ double wave_max(double v) {  // v >= 0
+  v = fmax(v, dpp<kRowShr1>(v));
+  v = fmax(v, dpp<kRowShr2>(v));
+  v = fmax(v, dpp<kRowShr4>(v));
+  v = fmax(v, dpp<kRowShr8>(v));
+  return fmax(fmax(readlane(v, 15), readlane(v, 31)), fmax(readlane(v, 47), readlane(v, 63)));
+}
+// lane i <- lane i-2 (0 for i < 2);  lane i <- lane i+2 (0 past the wave)
+__device__ __forceinline__ double shr2(double v) { return dpp<kWaveShr1>(dpp<kWaveShr1>(v)); }
+__device__ __forceinline__ double shl2(double v) { return dpp<kWaveShl1>(dpp<kWaveShl1>(v)); }
 __device__ __forceinline__ bool wave_any(bool b) { return __ballot(b) != 0ull; }
 
 __device__ __forceinline__ double limit_scaling(double v) {
@@ -122,7 +192,7 @@ __global__ __launch_bounds__(kWave) void k_build(mpcqp_params p, int B, const do
     rv = rb[4 * lane + 3];
   }
   // np.unwrap: ddmod = mod(dd + pi, 2pi) - pi; boundary fix; zero when |dd| < pi
-  const double prev = __shfl_up(ryaw, 1, kWave);
+  const double prev = dpp<kWaveShr1>(ryaw);
   double pc = 0.0;
   if (lane >= 1 && lane <= N) {
     const double dd = ryaw - prev;
@@ -134,7 +204,7 @@ __global__ __launch_bounds__(kWave) void k_build(mpcqp_params p, int B, const do
   // cumsum in numpy's sequential order (bit-exact)
   double cs = 0.0, mine = 0.0;
   for (int j = 1; j <= N; ++j) {
-    cs = cs + __shfl(pc, j, kWave);
+    cs = cs + readlane(pc, j);
     if (lane == j) mine = cs;
   }
   const double uyaw = lane == 0 ? ryaw : ryaw + mine;
@@ -145,9 +215,11 @@ __global__ __launch_bounds__(kWave) void k_build(mpcqp_params p, int B, const do
     mb[7 * N + 4 * lane + 3] = rv;
   }
   // linearisation point of step k: ref[max(k-1, 0)]
-  const int src = lane == 0 ? 0 : lane - 1;
-  const double psi = __shfl(uyaw, src, kWave);
-  const double v = __shfl(rv, src, kWave);
+  // (DPP must run with every lane active: an exec-masked source lane reads as 0)
+  const double psi_m1 = dpp<kWaveShr1>(uyaw);
+  const double v_m1 = dpp<kWaveShr1>(rv);
+  const double psi = lane == 0 ? uyaw : psi_m1;
+  const double v = lane == 0 ? rv : v_m1;
   if (lane < N) {
     const double dt = p.dt, L = p.wheelbase_px;
     const double sec2 = 1.0 / (1.0 * 1.0 + 1e-9);
@@ -167,40 +239,31 @@ __global__ __launch_bounds__(kWave) void k_build(mpcqp_params p, int B, const do
   if (lane >= 4 && lane < 6) mb[11 * N + 4 + lane] = u_prev ? u_prev[(size_t)b * 2 + lane - 4] : 0.0;
 }
 
-// ------------------------------------------------------------------ K2: solve
+// ------------------------------------------------------------------ K2a: setup
+// Condensing (states and slacks eliminated) + OSQP Ruiz/cost scaling.
 // Row slots owned by lane p (p < n = 2N):
 //   slot 0: v row (p even): v_{p/2+1} - v0 = dt * sum_{j<=p/2} a_j   (mpc_controller.py:81-82,115-116)
 //   slot 1: input row        U_p                                      (:83-86)
 //   slot 2: rate row         U_p - U_{p-2} (u_prev at k = 0)          (:89-106)
-// Everything below is in OSQP's scaled space: x = D^-1 U, rows E * (C U), cost c.
 template <int N>
-struct Solver {
+struct SetupSmem {
   static constexpr int n = 2 * N;
-  static constexpr int LD = n + 1;  // odd leading dimension: conflict-free row and column access
-  static constexpr int S = model_stride(N);
-
-  struct Smem {
-    double P[n * LD];   // scaled P = 2 c D H D
-    double buf[2 * kWave];  // broadcast vector (the sweep keeps a wrapped copy in [n, 2n))
-    double model[S];
-    double pre[4][N + 1];  // prefix sums of alpha, beta, gamma, eta
-    double err[N + 1][4];  // free-response tracking error e_m = sx_m - r_m
-    double sv[N + 1];      // suffix sums over v rows of E^2 * weight
-    double D[n];
-    double g[n];
-  };
+  static constexpr int LD = n + 1;  // odd: conflict-free row and column access
+  double P[n * LD];
+  double buf[kWave];
+  double model[model_stride(N)];
+  double pre[4][N + 1];  // prefix sums of alpha, beta, gamma, eta
+  double err[N + 1][4];  // free-response tracking error e_m = sx_m - r_m
+  double g[n];
 };
 
 template <int N>
-__global__ __launch_bounds__(kWave) void k_solve(mpcqp_params p, int B, const double* __restrict__ model,
-                                                 double* __restrict__ u0o, double* __restrict__ Xo,
-                                                 double* __restrict__ Uo, int32_t* __restrict__ statuso,
-                                                 int32_t* __restrict__ iterso, uint8_t* __restrict__ activeo) {
-  using Sv = Solver<N>;
-  constexpr int n = Sv::n;
-  constexpr int LD = Sv::LD;
-  constexpr int S = Sv::S;
-  __shared__ typename Sv::Smem sm;
+__global__ __launch_bounds__(kWave) void k_setup(mpcqp_params p, int B, const double* __restrict__ model,
+                                                 double* __restrict__ state) {
+  constexpr int n = 2 * N;
+  constexpr int LD = SetupSmem<N>::LD;
+  constexpr int S = model_stride(N);
+  __shared__ SetupSmem<N> sm;
   const int b = blockIdx.x;
   const int lane = threadIdx.x;
   if (b >= B) return;
@@ -209,7 +272,6 @@ __global__ __launch_bounds__(kWave) void k_solve(mpcqp_params p, int B, const do
   const int cc = lane & 1;  // 0 = acceleration, 1 = steering
   const double dt = p.dt;
 
-  // ---- stage the model in LDS (coalesced) ----
   {
     const double* mb = model + (size_t)b * S;
     for (int i = lane; i < S; i += kWave) sm.model[i] = mb[i];
@@ -226,7 +288,7 @@ __global__ __launch_bounds__(kWave) void k_solve(mpcqp_params p, int B, const do
   const double* x0 = sm.model + 11 * N + 4;
   const double* up = sm.model + 11 * N + 8;
 
-  // prefix sums (lane 0..3 one array each) and free response (lane 4)
+  // prefix sums (lanes 0..3, one array each) and free response (lane 4)
   if (lane < 4) {
     const double* a = sm.model + lane * N;
     double acc = 0.0;
@@ -359,7 +421,7 @@ __global__ __launch_bounds__(kWave) void k_solve(mpcqp_params p, int B, const do
   for (int it = 0; it < p.scaling; ++it) {
     // column norms of [P; A] (first n columns of the KKT matrix)
     const double sufE = rscan_max(E[0], lane);  // max E over v rows >= p/2 (odd lanes carry 0)
-    const double e2n = __shfl_down(E[2], 2, kWave);
+    const double e2n = shl2(E[2]);
     double ccol = fmax(E[1], E[2]);
     if (lane + 2 < n) ccol = fmax(ccol, e2n);
     if (even) ccol = fmax(ccol, dt * sufE);
@@ -367,10 +429,10 @@ __global__ __launch_bounds__(kWave) void k_solve(mpcqp_params p, int B, const do
     const double dl = act ? 1.0 / sqrt(limit_scaling(fmax(cmax, ccol))) : 0.0;
     // row norms of A
     const double preD = scan_max(even ? D : 0.0, lane);
-    const double Dm2 = __shfl_up(D, 2, kWave);
-    double el0 = even ? 1.0 / sqrt(limit_scaling(E[0] * dt * preD)) : 0.0;
-    double el1 = act ? 1.0 / sqrt(limit_scaling(E[1] * D)) : 0.0;
-    double el2 = act ? 1.0 / sqrt(limit_scaling(E[2] * (lane >= 2 ? fmax(D, Dm2) : D))) : 0.0;
+    const double Dm2 = shr2(D);
+    const double el0 = even ? 1.0 / sqrt(limit_scaling(E[0] * dt * preD)) : 0.0;
+    const double el1 = act ? 1.0 / sqrt(limit_scaling(E[1] * D)) : 0.0;
+    const double el2 = act ? 1.0 / sqrt(limit_scaling(E[2] * (lane >= 2 ? fmax(D, Dm2) : D))) : 0.0;
     // apply: P <- dl P dl (column `lane`), q <- dl q
     __syncthreads();
     sm.buf[lane] = dl;
@@ -401,6 +463,15 @@ __global__ __launch_bounds__(kWave) void k_solve(mpcqp_params p, int B, const do
     cmax = cm2 * ct;
     cscale *= ct;
   }
+  __syncthreads();
+
+  // ---- write the solver state ----
+  double* st = state + (size_t)b * state_stride(N);
+  if (act) {
+    // symmetric Pbar: the lower-triangle value (computed by column `min`) for both halves
+    for (int i = 0; i < n; ++i) st[i * n + lane] = i >= lane ? sm.P[i * LD + lane] : sm.P[lane * LD + i];
+  }
+  double* lf = st + state_lane_off(N);
   double wb[3];
 #pragma unroll
   for (int r = 0; r < 3; ++r) {
@@ -408,360 +479,512 @@ __global__ __launch_bounds__(kWave) void k_solve(mpcqp_params p, int B, const do
     hi[r] *= E[r];
     wb[r] = E[r] > 0.0 ? cscale * wt[r] / (E[r] * E[r]) : 0.0;
   }
-  __syncthreads();
-  if (act) sm.D[lane] = D;
-  __syncthreads();
+  lf[kFq * kWave + lane] = qv;
+  lf[kFD * kWave + lane] = D;
+  lf[kFx * kWave + lane] = 0.0;
+#pragma unroll
+  for (int r = 0; r < 3; ++r) {
+    lf[(kFE0 + r) * kWave + lane] = E[r];
+    lf[(kFlo0 + r) * kWave + lane] = lo[r];
+    lf[(kFhi0 + r) * kWave + lane] = hi[r];
+    lf[(kFw0 + r) * kWave + lane] = wb[r];
+  }
+  if (lane == 0) {
+    double* sc = st + state_scal_off(N);
+    sc[0] = cscale;
+    sc[1] = 0.0;  // admm_ok
+    sc[2] = 0.0;  // admm iterations
+    sc[3] = 0.0;  // factorizations
+  }
+}
 
-  // ---- structured operators ----
+// ------------------------------------------------------------------ shared solver context
+// Per-lane view of one scaled QP plus the structured operators and the KKT inverse.
+template <int N>
+struct Ctx {
+  static constexpr int n = 2 * N;
+  int lane;
+  bool act, even;
+  double dt;
+  double D, qv;
+  double E[3], lo[3], hi[3], wb[3];
+  double cscale;
+  const double* __restrict__ P;  // Pbar (global, L2-resident)
+  double* buf;                   // LDS broadcast buffer, >= 2*kWave doubles
+  double* sv;                    // LDS, N+1 doubles
+  double* Dl;                    // LDS copy of D (n doubles)
+  // KKT inverse, row `lane`: A^{-1}[lane][j] = -sig * r[j] (symmetric sweep operator, row scale sig)
+  double r[n];
+  double sig;
+
+  __device__ __forceinline__ void load(const double* st, int ln, double dt_, double* buf_, double* sv_, double* Dl_) {
+    lane = ln;
+    act = ln < n;
+    even = act && ((ln & 1) == 0);
+    dt = dt_;
+    buf = buf_;
+    sv = sv_;
+    Dl = Dl_;
+    P = st;
+    const double* lf = st + state_lane_off(N);
+    qv = lf[kFq * kWave + ln];
+    D = lf[kFD * kWave + ln];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      E[k] = lf[(kFE0 + k) * kWave + ln];
+      lo[k] = lf[(kFlo0 + k) * kWave + ln];
+      hi[k] = lf[(kFhi0 + k) * kWave + ln];
+      wb[k] = lf[(kFw0 + k) * kWave + ln];
+    }
+    cscale = st[state_scal_off(N)];
+    if (act) Dl[ln] = D;
+    __syncthreads();
+  }
+
+  // Make the per-lane problem data opaque to the optimizer at the top of a solver
+  // iteration: otherwise LICM hoists dozens of derived values (reciprocals, products,
+  // masks) out of the loops and the kernel drops to one wave per SIMD.
+  __device__ __forceinline__ void opaque() {
+    asm volatile("" : "+v"(D), "+v"(qv), "+v"(lane));
+    asm volatile("" : "+v"(E[0]), "+v"(E[1]), "+v"(E[2]));
+    asm volatile("" : "+v"(lo[0]), "+v"(lo[1]), "+v"(lo[2]));
+    asm volatile("" : "+v"(hi[0]), "+v"(hi[1]), "+v"(hi[2]));
+    asm volatile("" : "+v"(wb[0]), "+v"(wb[1]), "+v"(wb[2]));
+  }
+
   // z = Cbar x
-  auto Cmul = [&](double x, double z[3]) {
+  __device__ __forceinline__ void Cmul(double x, double z[3]) const {
     const double t = D * x;
-    const double pre = scan_sum(even ? t : 0.0, lane);
-    const double tm2 = __shfl_up(t, 2, kWave);
+    const double pre = scan_add(even ? t : 0.0, lane);
+    const double tm2 = shr2(t);
     z[0] = E[0] * dt * pre;
     z[1] = E[1] * t;
     z[2] = E[2] * (lane >= 2 ? t - tm2 : t);
-  };
+  }
   // x = Cbar' y
-  auto CTmul = [&](const double y[3]) -> double {
-    const double suf = rscan_sum(E[0] * y[0], lane);
+  __device__ __forceinline__ double CTmul(const double y[3]) const {
+    const double suf = rscan_add(E[0] * y[0], lane);
     const double ey2 = E[2] * y[2];
-    const double n2 = __shfl_down(ey2, 2, kWave);
+    const double n2 = shl2(ey2);
     double t = (even ? dt * suf : 0.0) + E[1] * y[1] + ey2;
     if (lane + 2 < n) t -= n2;
     return act ? D * t : 0.0;
-  };
-  // (Pbar v)_lane
-  auto Pmul = [&](double v) -> double {
+  }
+  // broadcast v (one value per lane) through LDS
+  __device__ __forceinline__ void put(double v) const {
     __syncthreads();
-    sm.buf[lane] = act ? v : 0.0;
+    buf[lane] = act ? v : 0.0;
     __syncthreads();
-    double acc = 0.0;
-    if (act) {
-#pragma unroll 8
-      for (int j = 0; j < n; ++j) acc += sm.P[lane * LD + j] * sm.buf[j];
+  }
+  // (Pbar v)_lane, Pbar symmetric: column reads are coalesced
+  __device__ __forceinline__ double Pmul(double v) const {
+    put(v);
+    const int col = act ? lane : 0;
+    double acc0 = 0.0, acc1 = 0.0;
+#pragma unroll
+    for (int j0 = 0; j0 < n; j0 += kChunk) {
+      double pv[kChunk], bv[kChunk];
+#pragma unroll
+      for (int t = 0; t < kChunk; ++t)
+        if (j0 + t < n) {
+          pv[t] = P[(j0 + t) * n + col];
+          bv[t] = buf[j0 + t];
+        }
+#pragma unroll
+      for (int t = 0; t < kChunk; t += 2) {
+        if (j0 + t < n) acc0 = fma(pv[t], bv[t], acc0);
+        if (j0 + t + 1 < n) acc1 = fma(pv[t + 1], bv[t + 1], acc1);
+      }
+      __builtin_amdgcn_sched_barrier(0);
     }
-    return acc;
-  };
-
-  // ---- KKT matrix rows in registers: A = Pbar + sig I + Cbar' diag(rw) Cbar ----
-  // Row `lane` lives in a[]; the sweep below rotates it left once per pivot so
-  // that every register index is static while the pivot loop stays rolled.
-  double a[n];
-  auto form_rows = [&](double sig, const double rw[3]) {
-    // Opaque copy of the lane id: keeps the per-column masks and LDS addresses
-    // below from being hoisted out of the solver loop (they would pin ~100 VGPRs).
+    return act ? acc0 + acc1 : 0.0;
+  }
+  // KKT matrix A = Pbar + s I + Cbar' diag(rw) Cbar, row `lane` -> r[] (sig = 1)
+  __device__ __forceinline__ void form(double s, const double rw[3]) {
+    // opaque lane copy: keeps per-column masks/addresses from being hoisted out of solver loops
     int ln = lane;
     asm volatile("" : "+v"(ln));
     const bool ev_ln = ln < n && (ln & 1) == 0;
-    __syncthreads();
     const double ev = E[0] * E[0] * rw[0];
-    const double suf = rscan_sum(even ? ev : 0.0, lane);  // sum over v rows >= lane/2
-    if (even) sm.sv[lane >> 1] = suf;
+    const double suf = rscan_add(even ? ev : 0.0, lane);  // sum over v rows >= lane/2
     const double du2 = E[2] * E[2] * rw[2];
-    const double du2n = __shfl_down(du2, 2, kWave);
+    const double du2n = shl2(du2);
+    __syncthreads();
+    if (even) sv[lane >> 1] = suf;
     __syncthreads();
     double diag = E[1] * E[1] * rw[1] + du2;
     if (ln + 2 < n) diag += du2n;
-    const int lrow = ln < n ? ln : 0;
+    const int col = ln < n ? ln : 0;
 #pragma unroll
     for (int j = 0; j < n; ++j) {
       double t = 0.0;
       if ((j & 1) == 0 && ev_ln) {
         const int mx = (ln > j ? ln : j) >> 1;
-        t = dt * dt * sm.sv[mx];
+        t = dt * dt * sv[mx];
       }
       if (j == ln) t += diag;
       if (j == ln + 2) t -= du2n;
       if (j + 2 == ln) t -= du2;
-      const double v = sm.P[lrow * LD + j] + D * sm.D[j] * t + (j == ln ? sig : 0.0);
-      a[j] = ln < n ? v : 0.0;
+      const double v = P[j * n + col] + D * Dl[j] * t + (j == ln ? s : 0.0);
+      r[j] = ln < n ? v : 0.0;
+      if ((j % kChunk) == kChunk - 1) __builtin_amdgcn_sched_barrier(0);
     }
-  };
-  // symmetric sweep operator: a <- -A^{-1} (row `lane`).  false on a non-positive pivot.
-  auto sweep = [&]() -> bool {
+    sig = 1.0;
+  }
+  // Symmetric sweep operator on the rows in r[]: afterwards A^{-1} = -sig * r (row `lane`).
+  // The pivot row of step k is a scalar multiple of its own row (symmetry), so it is carried
+  // in `sig` and every step is n uniform FMAs (no per-element select for the pivot lane).
+  // The pivot loop is unrolled at compile time (sweep_step<K>) so every register index is
+  // static and the row is updated in place.  false on a non-positive pivot.
+  // Symmetric sweep operator on the rows in r[]: afterwards A^{-1} = -sig * r (row `lane`).
+  // The pivot row of step k is a scalar multiple of its own row (symmetry), so it is carried
+  // in `sig` and every step is n uniform FMAs (no per-element select for the pivot lane).
+  // The row rotates one slot per step, so the pivot slot is always r[0] and the pivot loop
+  // stays rolled (static register indices).  false on a non-positive pivot.
+  __device__ __forceinline__ bool sweep() {
     bool ok = true;
     for (int k = 0; k < n; ++k) {
       __syncthreads();
-      sm.buf[lane] = a[0];  // column k == row k (symmetry); slot 0 holds absolute column k
-      if (lane < n) sm.buf[lane + n] = a[0];
+      const double colk = sig * r[0];
+      buf[lane] = colk;
+      if (lane < n) buf[lane + n] = colk;  // wrapped copy: buf[i + n] == buf[i]
       __syncthreads();
-      const double d = sm.buf[k];
+      const double d = buf[k];
       ok = ok && (d > 0.0) && isfinite(d);
       const double inv = 1.0 / d;
       const bool piv = lane == k;
-      double f = a[0] * inv;
-      if (piv) {
+      const double c = piv ? 0.0 : r[0] * inv;
+      const double* colv = buf + k;
 #pragma unroll
-        for (int j = 1; j < n; ++j) a[j] = 0.0;
-        f = -inv;
+      for (int j0 = 1; j0 < n; j0 += kChunk) {
+        double bv[kChunk];
+#pragma unroll
+        for (int t = 0; t < kChunk; ++t)
+          if (j0 + t < n) bv[t] = colv[j0 + t];
+#pragma unroll
+        for (int t = 0; t < kChunk; ++t)
+          if (j0 + t < n) r[j0 + t - 1] = fma(-c, bv[t], r[j0 + t]);
+        __builtin_amdgcn_sched_barrier(0);
       }
-      const double* col = sm.buf + k;  // col[j] = A[k][(k + j) mod n]
-#pragma unroll
-      for (int j = 1; j < n; ++j) a[j - 1] = fma(-f, col[j], a[j]);
-      a[n - 1] = piv ? -inv : f;
+      r[n - 1] = piv ? -1.0 / sig : c;
+      sig = piv ? sig * inv : sig;
     }
     return ok;
-  };
-  // -(a . v) with v broadcast through LDS == (A^{-1} v)_lane
-  auto inv_mul = [&](double v) -> double {
-    __syncthreads();
-    sm.buf[lane] = act ? v : 0.0;
-    __syncthreads();
+  }
+  // (A^{-1} v)_lane
+  __device__ __forceinline__ double inv_mul(double v) const {
+    put(v);
     double acc0 = 0.0, acc1 = 0.0;
 #pragma unroll
-    for (int j = 0; j < n; j += 2) {
-      acc0 = fma(a[j], sm.buf[j], acc0);
-      if (j + 1 < n) acc1 = fma(a[j + 1], sm.buf[j + 1], acc1);
+    for (int j0 = 0; j0 < n; j0 += kChunk) {
+      double bv[kChunk];
+#pragma unroll
+      for (int t = 0; t < kChunk; ++t)
+        if (j0 + t < n) bv[t] = buf[j0 + t];
+#pragma unroll
+      for (int t = 0; t < kChunk; t += 2) {
+        if (j0 + t < n) acc0 = fma(r[j0 + t], bv[t], acc0);
+        if (j0 + t + 1 < n) acc1 = fma(r[j0 + t + 1], bv[t + 1], acc1);
+      }
+      __builtin_amdgcn_sched_barrier(0);
     }
-    return act ? -(acc0 + acc1) : 0.0;
-  };
+    return act ? -sig * (acc0 + acc1) : 0.0;
+  }
+};
 
-  // ---- solver state ----
-  double x = 0.0;
-  double z[3] = {0.0, 0.0, 0.0}, y[3] = {0.0, 0.0, 0.0};
-  bool bad = false, admm_ok = false, pol_ok = false;
-  int admm_it = 0, pol_it = 0, n_fact = 0, n_ls = 0;
-  const bool use_admm = p.method == MPCQP_METHOD_ADMM;
-  const bool do_polish = (p.method == MPCQP_METHOD_NEWTON) || (p.polish != 0);
+template <int N>
+struct SolveSmem {
+  double buf[2 * kWave];
+  double sv[N + 1];
+  double Dl[2 * N];
+};
+
+// ------------------------------------------------------------------ K2b: ADMM
+template <int N>
+__global__ __launch_bounds__(kWave) void k_admm(mpcqp_params p, int B, double* __restrict__ state) {
+  __shared__ SolveSmem<N> sm;
+  const int b = blockIdx.x;
+  if (b >= B) return;
+  double* st = state + (size_t)b * state_stride(N);
+  Ctx<N> C;
+  C.load(st, threadIdx.x, p.dt, sm.buf, sm.sv, sm.Dl);
+  const bool act = C.act;
+  double x = 0.0, z[3] = {0.0, 0.0, 0.0}, y[3] = {0.0, 0.0, 0.0};
   double rho = p.rho;
-  const double sig = p.sigma, alpha = p.alpha;
-  double x_admm = 0.0;
-  // polish state
-  double zc[3] = {0.0, 0.0, 0.0};
-  int cd[3] = {0, 0, 0};
-  // phase 0 = ADMM, 1 = polish, 2 = done
-  int phase = use_admm ? 0 : (do_polish ? 1 : 2);
-  auto enter_polish = [&]() {
-    x_admm = x;
-    Cmul(x, zc);
-#pragma unroll
-    for (int r = 0; r < 3; ++r) cd[r] = zc[r] > hi[r] ? 2 : (zc[r] < lo[r] ? 1 : 0);
-  };
-  if (phase == 1) enter_polish();
-  int it = 0;
-  while (phase < 2) {
-    // ---- (re)factor: the single inlined instance of form_rows + sweep ----
-    double rw[3], tmp[3];
-    if (phase == 0) {
-      rw[0] = rw[1] = rw[2] = rho;
-    } else {
-#pragma unroll
-      for (int r = 0; r < 3; ++r) rw[r] = cd[r] ? 2.0 * wb[r] : 0.0;
-    }
-    form_rows(phase == 0 ? sig : 0.0, rw);
-    ++n_fact;
-    if (wave_any(!sweep())) {
-      bad = true;
-      break;
-    }
-    if (phase == 0) {
-      // ---- ADMM iterations with the current KKT inverse ----
-      bool refactor = false;
-      while (!refactor && it < p.max_iter) {
-        ++it;
-#pragma unroll
-        for (int r = 0; r < 3; ++r) tmp[r] = rho * z[r] - y[r];
-        const double rhs = CTmul(tmp) + sig * x - qv;
-        const double xt = inv_mul(rhs);
-        double zt[3];
-        Cmul(xt, zt);
-        x = alpha * xt + (1.0 - alpha) * x;
-        const double ir = 1.0 / rho;
-#pragma unroll
-        for (int r = 0; r < 3; ++r) {
-          const double v = alpha * zt[r] + (1.0 - alpha) * z[r];
-          const double vv = v + y[r] * ir;
-          double zn = vv;
-          if (vv > hi[r])
-            zn = (rho * vv + 2.0 * wb[r] * hi[r]) / (rho + 2.0 * wb[r]);
-          else if (vv < lo[r])
-            zn = (rho * vv + 2.0 * wb[r] * lo[r]) / (rho + 2.0 * wb[r]);
-          y[r] = y[r] + rho * (v - zn);
-          z[r] = zn;
-        }
-        admm_it = it;
-        if (it % p.check_termination == 0 || it == p.max_iter) {
-          double Ax[3];
-          Cmul(x, Ax);
-          const double Px = Pmul(x);
-          const double Aty = CTmul(y);
-          double pr = 0, nAx = 0, nz = 0, spr = 0, snAx = 0, snz = 0;
-#pragma unroll
-          for (int r = 0; r < 3; ++r) {
-            if (E[r] > 0.0) {
-              const double ie = 1.0 / E[r];
-              pr = fmax(pr, fabs((Ax[r] - z[r]) * ie));
-              nAx = fmax(nAx, fabs(Ax[r] * ie));
-              nz = fmax(nz, fabs(z[r] * ie));
-              spr = fmax(spr, fabs(Ax[r] - z[r]));
-              snAx = fmax(snAx, fabs(Ax[r]));
-              snz = fmax(snz, fabs(z[r]));
-            }
-          }
-          double du = 0, nPx = 0, nAty = 0, nq = 0, sdu = 0, snPx = 0, snAty = 0, snq = 0;
-          if (act) {
-            const double id = 1.0 / D;
-            const double rd = Px + qv + Aty;
-            du = fabs(rd * id);
-            nPx = fabs(Px * id);
-            nAty = fabs(Aty * id);
-            nq = fabs(qv * id);
-            sdu = fabs(rd);
-            snPx = fabs(Px);
-            snAty = fabs(Aty);
-            snq = fabs(qv);
-          }
-          pr = wave_max(pr);
-          nAx = wave_max(nAx);
-          nz = wave_max(nz);
-          du = wave_max(du);
-          nPx = wave_max(nPx);
-          nAty = wave_max(nAty);
-          nq = wave_max(nq);
-          const double ic = 1.0 / cscale;
-          du *= ic;
-          const double ep = p.eps_abs + p.eps_rel * fmax(nAx, nz);
-          const double ed = p.eps_abs + p.eps_rel * fmax(fmax(nPx, nAty), nq) * ic;
-          if (!isfinite(pr) || !isfinite(du)) {
-            bad = true;
-            break;
-          }
-          if (pr <= ep && du <= ed) {
-            admm_ok = true;
-            break;
-          }
-          if (p.adaptive_rho && it % p.adaptive_rho_interval == 0) {
-            spr = wave_max(spr);
-            snAx = wave_max(snAx);
-            snz = wave_max(snz);
-            sdu = wave_max(sdu);
-            snPx = wave_max(snPx);
-            snAty = wave_max(snAty);
-            snq = wave_max(snq);
-            const double pn = spr / (fmax(snAx, snz) + kDivTol);
-            const double dn = sdu / (fmax(fmax(snPx, snAty), snq) + kDivTol);
-            double rn = rho * sqrt(pn / (dn + kDivTol));
-            rn = fmin(fmax(rn, kRhoMin), kRhoMax);
-            if (rn > rho * p.adaptive_rho_tolerance || rn < rho / p.adaptive_rho_tolerance) {
-              rho = rn;
-              refactor = true;
-            }
-          }
-        }
+  const double sg = p.sigma, alpha = p.alpha;
+  bool bad = false, ok = false;
+  int it = 0, nfact = 0;
+  while (it < p.max_iter && !bad && !ok) {
+    {
+      const double rw[3] = {rho, rho, rho};
+      C.form(sg, rw);
+      ++nfact;
+      if (wave_any(!C.sweep())) {
+        bad = true;
+        break;
       }
-      if (bad) break;
-      if (!refactor) {  // converged or out of iterations
-        if (do_polish) {
-          enter_polish();
-          phase = 1;
-        } else {
-          phase = 2;
-        }
-      }
-      continue;
     }
-    // ---- polish step with the inverse of M = Pbar + sum_act 2 w C_r C_r' ----
-    ++pol_it;
-#pragma unroll
-    for (int r = 0; r < 3; ++r) tmp[r] = cd[r] == 2 ? rw[r] * hi[r] : (cd[r] == 1 ? rw[r] * lo[r] : 0.0);
-    const double rhs = CTmul(tmp) - qv;
-    double xn = inv_mul(rhs);
-    {  // one step of iterative refinement: res = rhs - M xn
-      double zz[3], t3[3];
-      Cmul(xn, zz);
-#pragma unroll
-      for (int r = 0; r < 3; ++r) t3[r] = rw[r] * zz[r];
-      const double Mx = Pmul(xn) + CTmul(t3);
-      xn += inv_mul(rhs - Mx);
-    }
-    double zn[3];
-    Cmul(xn, zn);
-    bool diff = false;
+    bool refactor = false;
+    double prox_a[3], prox_b[3];  // zn = (rho vv + 2 w bnd) / (rho + 2 w)
 #pragma unroll
     for (int r = 0; r < 3; ++r) {
-      const int c2 = zn[r] > hi[r] ? 2 : (zn[r] < lo[r] ? 1 : 0);
-      diff = diff || (c2 != cd[r]);
+      prox_a[r] = rho / (rho + 2.0 * C.wb[r]);
+      prox_b[r] = 2.0 * C.wb[r] / (rho + 2.0 * C.wb[r]);
     }
-    if (!wave_any(diff)) {
-      x = xn;
-      pol_ok = true;
-      phase = 2;
-      continue;
-    }
-    // Armijo backtracking on the scaled objective along d = xn - x
-    const double dx = act ? xn - x : 0.0;
-    const double Px = Pmul(x);
-    const double Pd = Pmul(dx);
-    double zd[3], gt[3];
+    const double ir = 1.0 / rho;
+    while (!refactor && it < p.max_iter) {
+      ++it;
+      C.opaque();
+      double tmp[3];
 #pragma unroll
-    for (int r = 0; r < 3; ++r) {
-      zd[r] = zn[r] - zc[r];
-      const double res = zc[r] > hi[r] ? zc[r] - hi[r] : (zc[r] < lo[r] ? zc[r] - lo[r] : 0.0);
-      gt[r] = 2.0 * wb[r] * res;
-    }
-    const double gr = CTmul(gt);
-    const double slope = wave_sum(act ? (Px + qv + gr) * dx : 0.0);
-    const double qd = wave_sum(act ? dx * Pd : 0.0);
-    const double lin = wave_sum(act ? (Px + qv) * dx : 0.0);
-    const double q0 = wave_sum(act ? x * (0.5 * Px + qv) : 0.0);
-    auto pen = [&](double t) -> double {
-      double s = 0.0;
+      for (int r = 0; r < 3; ++r) tmp[r] = rho * z[r] - y[r];
+      const double rhs = C.CTmul(tmp) + sg * x - C.qv;
+      const double xt = C.inv_mul(rhs);
+      double zt[3];
+      C.Cmul(xt, zt);
+      x = alpha * xt + (1.0 - alpha) * x;
 #pragma unroll
       for (int r = 0; r < 3; ++r) {
-        const double zt = zc[r] + t * zd[r];
-        const double d = zt > hi[r] ? zt - hi[r] : (zt < lo[r] ? lo[r] - zt : 0.0);
-        s += wb[r] * d * d;
+        const double v = alpha * zt[r] + (1.0 - alpha) * z[r];
+        const double vv = v + y[r] * ir;
+        double zn = vv;
+        if (vv > C.hi[r])
+          zn = prox_a[r] * vv + prox_b[r] * C.hi[r];
+        else if (vv < C.lo[r])
+          zn = prox_a[r] * vv + prox_b[r] * C.lo[r];
+        y[r] = y[r] + rho * (v - zn);
+        z[r] = zn;
       }
-      return wave_sum(s);
-    };
-    const double f0 = q0 + pen(0.0);
-    double t = 1.0;
-    for (int ls = 0; ls < 60; ++ls) {
-      ++n_ls;
-      const double ft = q0 + t * lin + 0.5 * t * t * qd + pen(t);
-      if (ft <= f0 + 1e-4 * t * slope) break;
-      t *= 0.5;
-    }
-    x = x + t * dx;
-    Cmul(x, zc);
+      if (it % p.check_termination == 0 || it == p.max_iter) {
+        double Ax[3];
+        C.Cmul(x, Ax);
+        const double Px = C.Pmul(x);
+        const double Aty = C.CTmul(y);
+        double pr = 0, nAx = 0, nz = 0, spr = 0, snAx = 0, snz = 0;
 #pragma unroll
-    for (int r = 0; r < 3; ++r) cd[r] = zc[r] > hi[r] ? 2 : (zc[r] < lo[r] ? 1 : 0);
-    if (pol_it >= p.polish_max_iter) phase = 2;
+        for (int r = 0; r < 3; ++r) {
+          if (C.E[r] > 0.0) {
+            const double ie = 1.0 / C.E[r];
+            pr = fmax(pr, fabs((Ax[r] - z[r]) * ie));
+            nAx = fmax(nAx, fabs(Ax[r] * ie));
+            nz = fmax(nz, fabs(z[r] * ie));
+            spr = fmax(spr, fabs(Ax[r] - z[r]));
+            snAx = fmax(snAx, fabs(Ax[r]));
+            snz = fmax(snz, fabs(z[r]));
+          }
+        }
+        double du = 0, nPx = 0, nAty = 0, nq = 0, sdu = 0, snPx = 0, snAty = 0, snq = 0;
+        if (act) {
+          const double id = 1.0 / C.D;
+          const double rd = Px + C.qv + Aty;
+          du = fabs(rd * id);
+          nPx = fabs(Px * id);
+          nAty = fabs(Aty * id);
+          nq = fabs(C.qv * id);
+          sdu = fabs(rd);
+          snPx = fabs(Px);
+          snAty = fabs(Aty);
+          snq = fabs(C.qv);
+        }
+        pr = wave_max(pr);
+        nAx = wave_max(nAx);
+        nz = wave_max(nz);
+        du = wave_max(du);
+        nPx = wave_max(nPx);
+        nAty = wave_max(nAty);
+        nq = wave_max(nq);
+        const double ic = 1.0 / C.cscale;
+        du *= ic;
+        const double ep = p.eps_abs + p.eps_rel * fmax(nAx, nz);
+        const double ed = p.eps_abs + p.eps_rel * fmax(fmax(nPx, nAty), nq) * ic;
+        if (!isfinite(pr) || !isfinite(du)) {
+          bad = true;
+          break;
+        }
+        if (pr <= ep && du <= ed) {
+          ok = true;
+          break;
+        }
+        if (p.adaptive_rho && it % p.adaptive_rho_interval == 0) {
+          spr = wave_max(spr);
+          snAx = wave_max(snAx);
+          snz = wave_max(snz);
+          sdu = wave_max(sdu);
+          snPx = wave_max(snPx);
+          snAty = wave_max(snAty);
+          snq = wave_max(snq);
+          const double pn = spr / (fmax(snAx, snz) + kDivTol);
+          const double dn = sdu / (fmax(fmax(snPx, snAty), snq) + kDivTol);
+          double rn = rho * sqrt(pn / (dn + kDivTol));
+          rn = fmin(fmax(rn, kRhoMin), kRhoMax);
+          if (rn > rho * p.adaptive_rho_tolerance || rn < rho / p.adaptive_rho_tolerance) {
+            rho = rn;
+            refactor = true;
+          }
+        }
+      }
+    }
   }
-  int st;
+  double* lf = st + state_lane_off(N);
+  lf[kFx * kWave + threadIdx.x] = act ? x : 0.0;
+  if (threadIdx.x == 0) {
+    double* sc = st + state_scal_off(N);
+    sc[1] = bad ? -1.0 : (ok ? 1.0 : 0.0);
+    sc[2] = (double)it;
+    sc[3] = (double)nfact;
+  }
+}
+
+// ------------------------------------------------------------------ K2c: polish + outputs
+template <int N>
+__global__ __launch_bounds__(kWave) void k_finish(mpcqp_params p, int B, const double* __restrict__ model,
+                                                  const double* __restrict__ state, double* __restrict__ u0o,
+                                                  double* __restrict__ Xo, double* __restrict__ Uo,
+                                                  int32_t* __restrict__ statuso, int32_t* __restrict__ iterso,
+                                                  uint8_t* __restrict__ activeo) {
+  constexpr int n = 2 * N;
+  __shared__ SolveSmem<N> sm;
+  const int b = blockIdx.x;
+  if (b >= B) return;
+  const int lane = threadIdx.x;
+  const double* st = state + (size_t)b * state_stride(N);
+  Ctx<N> C;
+  C.load(st, lane, p.dt, sm.buf, sm.sv, sm.Dl);
+  const bool act = C.act;
+  const bool use_admm = p.method == MPCQP_METHOD_ADMM;
+  const bool do_polish = !use_admm || p.polish != 0;
+  const double* sc = st + state_scal_off(N);
+  const double admm_flag = use_admm ? sc[1] : 0.0;
+  bool bad = admm_flag < 0.0;
+  const bool admm_ok = admm_flag > 0.0;
+  const int admm_it = use_admm ? (int)sc[2] : 0;
+  int nfact = use_admm ? (int)sc[3] : 0;
+  double x = use_admm ? st[state_lane_off(N) + kFx * kWave + lane] : 0.0;
+  const double x_admm = x;
+  bool pol_ok = false;
+  int pol_it = 0, n_ls = 0;
+
+  if (do_polish && !bad) {
+    double zc[3];
+    int cd[3];
+    C.Cmul(x, zc);
+#pragma unroll
+    for (int r = 0; r < 3; ++r) cd[r] = zc[r] > C.hi[r] ? 2 : (zc[r] < C.lo[r] ? 1 : 0);
+    while (pol_it < p.polish_max_iter) {
+      ++pol_it;
+      C.opaque();
+      double rw[3], tmp[3];
+#pragma unroll
+      for (int r = 0; r < 3; ++r) {
+        rw[r] = cd[r] ? 2.0 * C.wb[r] : 0.0;
+        tmp[r] = cd[r] == 2 ? rw[r] * C.hi[r] : (cd[r] == 1 ? rw[r] * C.lo[r] : 0.0);
+      }
+      C.form(0.0, rw);
+      ++nfact;
+      if (wave_any(!C.sweep())) {
+        bad = true;
+        break;
+      }
+      const double rhs = C.CTmul(tmp) - C.qv;
+      double xn = C.inv_mul(rhs);
+      {  // one step of iterative refinement: res = rhs - M xn
+        double zz[3], t3[3];
+        C.Cmul(xn, zz);
+#pragma unroll
+        for (int r = 0; r < 3; ++r) t3[r] = rw[r] * zz[r];
+        const double Mx = C.Pmul(xn) + C.CTmul(t3);
+        xn += C.inv_mul(rhs - Mx);
+      }
+      double zn[3];
+      C.Cmul(xn, zn);
+      bool diff = false;
+#pragma unroll
+      for (int r = 0; r < 3; ++r) {
+        const int c2 = zn[r] > C.hi[r] ? 2 : (zn[r] < C.lo[r] ? 1 : 0);
+        diff = diff || (c2 != cd[r]);
+      }
+      if (!wave_any(diff)) {
+        x = xn;
+        pol_ok = true;
+        break;
+      }
+      // Armijo backtracking on the scaled objective along d = xn - x
+      const double dx = act ? xn - x : 0.0;
+      const double Px = C.Pmul(x);
+      const double Pd = C.Pmul(dx);
+      double zd[3], gt[3];
+#pragma unroll
+      for (int r = 0; r < 3; ++r) {
+        zd[r] = zn[r] - zc[r];
+        const double res = zc[r] > C.hi[r] ? zc[r] - C.hi[r] : (zc[r] < C.lo[r] ? zc[r] - C.lo[r] : 0.0);
+        gt[r] = 2.0 * C.wb[r] * res;
+      }
+      const double gr = C.CTmul(gt);
+      const double slope = wave_sum(act ? (Px + C.qv + gr) * dx : 0.0);
+      const double qd = wave_sum(act ? dx * Pd : 0.0);
+      const double lin = wave_sum(act ? (Px + C.qv) * dx : 0.0);
+      const double q0 = wave_sum(act ? x * (0.5 * Px + C.qv) : 0.0);
+      auto pen = [&](double t) -> double {
+        double s = 0.0;
+#pragma unroll
+        for (int r = 0; r < 3; ++r) {
+          const double zt = zc[r] + t * zd[r];
+          const double d = zt > C.hi[r] ? zt - C.hi[r] : (zt < C.lo[r] ? C.lo[r] - zt : 0.0);
+          s += C.wb[r] * d * d;
+        }
+        return wave_sum(s);
+      };
+      const double f0 = q0 + pen(0.0);
+      double t = 1.0;
+      for (int ls = 0; ls < 60; ++ls) {
+        ++n_ls;
+        const double ft = q0 + t * lin + 0.5 * t * t * qd + pen(t);
+        if (ft <= f0 + 1e-4 * t * slope) break;
+        t *= 0.5;
+      }
+      x = x + t * dx;
+      C.Cmul(x, zc);
+#pragma unroll
+      for (int r = 0; r < 3; ++r) cd[r] = zc[r] > C.hi[r] ? 2 : (zc[r] < C.lo[r] ? 1 : 0);
+    }
+  }
+  int status;
   if (bad) {
-    st = MPCQP_NUMERICAL_ERROR;
+    status = MPCQP_NUMERICAL_ERROR;
   } else if (pol_ok) {
-    st = MPCQP_SOLVED;
+    status = MPCQP_SOLVED;
   } else if (use_admm) {
     if (do_polish) x = x_admm;  // polish failed: return the ADMM iterate (OSQP behaviour)
-    st = admm_ok ? (do_polish ? MPCQP_SOLVED_INACCURATE : MPCQP_SOLVED) : MPCQP_MAX_ITER_REACHED;
+    status = admm_ok ? (do_polish ? MPCQP_SOLVED_INACCURATE : MPCQP_SOLVED) : MPCQP_MAX_ITER_REACHED;
   } else {
-    st = MPCQP_MAX_ITER_REACHED;
+    status = MPCQP_MAX_ITER_REACHED;
   }
 
   // ---- outputs (unscaled) ----
-  const double U = act ? D * x : 0.0;
+  const double* mb = model + (size_t)b * model_stride(N);
+  const int cc = lane & 1;
+  const double U = act ? C.D * x : 0.0;
+  const double dt = p.dt;
+  const double x00 = mb[11 * N + 4], x01 = mb[11 * N + 5], x02 = mb[11 * N + 6], x03 = mb[11 * N + 7];
+  const double up0 = mb[11 * N + 8], up1 = mb[11 * N + 9];
+  const double sj = act ? mb[4 * N + (lane >> 1)] : 0.0;
   // v_{j+1} on lane 2j, psi_{j+1} on lane 2j+1
-  const double vacc = scan_sum(even ? U : 0.0, lane);
-  const double sacc = scan_sum((act && cc == 1) ? si[lane >> 1] * U : 0.0, lane);
+  const double vacc = scan_add(C.even ? U : 0.0, lane);
+  const double sacc = scan_add((act && cc == 1) ? sj * U : 0.0, lane);
   // lane k <- (psi_k, v_k)
   const int srcv = lane == 0 ? 0 : 2 * (lane - 1);
   const double vk_s = __shfl(vacc, srcv < kWave ? srcv : 0, kWave);
   const double pk_s = __shfl(sacc, (srcv + 1) < kWave ? srcv + 1 : 0, kWave);
-  const double vk = lane == 0 ? x0[3] : x0[3] + dt * vk_s;
-  const double pk = lane == 0 ? x0[2] : x0[2] + pk_s;
+  const double vk = lane == 0 ? x03 : x03 + dt * vk_s;
+  const double pk = lane == 0 ? x02 : x02 + pk_s;
   double t0 = 0.0, t1 = 0.0;
   if (lane < N) {
-    t0 = al[lane] * pk + be[lane] * vk + c0[lane];
-    t1 = ga[lane] * pk + et[lane] * vk + c1[lane];
+    t0 = mb[lane] * pk + mb[N + lane] * vk + mb[5 * N + lane];
+    t1 = mb[2 * N + lane] * pk + mb[3 * N + lane] * vk + mb[6 * N + lane];
   }
-  const double in0 = scan_sum(t0, lane), in1 = scan_sum(t1, lane);
-  const double ex0 = __shfl_up(in0, 1, kWave), ex1 = __shfl_up(in1, 1, kWave);  // exclusive prefix
-  const double sx0 = lane == 0 ? 0.0 : ex0;
-  const double sx1 = lane == 0 ? 0.0 : ex1;
-  const double Xk0 = x0[0] + sx0, Xk1 = x0[1] + sx1;
+  const double in0 = scan_add(t0, lane), in1 = scan_add(t1, lane);
+  const double ex0 = dpp<kWaveShr1>(in0), ex1 = dpp<kWaveShr1>(in1);  // exclusive prefix
+  const double Xk0 = x00 + ex0, Xk1 = x01 + ex1;
   if (Xo && lane <= N) {
     double* Xb = Xo + (size_t)b * 4 * (N + 1);
     Xb[0 * (N + 1) + lane] = Xk0;
@@ -771,50 +994,76 @@ __global__ __launch_bounds__(kWave) void k_solve(mpcqp_params p, int B, const do
   }
   if (Uo && act) Uo[(size_t)b * n + cc * N + (lane >> 1)] = U;
   if (u0o && lane < 2) u0o[(size_t)b * 2 + lane] = U;
+  const double Um2 = shr2(U);
   if (activeo) {
     uint8_t* ab = activeo + (size_t)b * (5 * N + 1);
     if (lane <= N) ab[lane] = vk > p.v_bounds[1] ? 2 : (vk < p.v_bounds[0] ? 1 : 0);
-    const double Um2 = __shfl_up(U, 2, kWave);
     if (act) {
       ab[N + 1 + lane] = U > p.u_bounds[2 * cc + 1] ? 2 : (U < p.u_bounds[2 * cc] ? 1 : 0);
-      const double d = U - (lane < 2 ? up[cc] : Um2);
+      const double d = U - (lane < 2 ? (cc ? up1 : up0) : Um2);
       ab[3 * N + 1 + lane] = d > p.du_bounds[2 * cc + 1] ? 2 : (d < p.du_bounds[2 * cc] ? 1 : 0);
     }
   }
   if (lane == 0) {
-    statuso[b] = st;
+    statuso[b] = status;
     if (iterso) {
       iterso[4 * (size_t)b + 0] = admm_it;
       iterso[4 * (size_t)b + 1] = pol_it;
-      iterso[4 * (size_t)b + 2] = n_fact;
+      iterso[4 * (size_t)b + 2] = nfact;
       iterso[4 * (size_t)b + 3] = n_ls;
     }
   }
 }
 
-// ------------------------------------------------------------------ dispatch
-using solve_fn = void (*)(mpcqp_params, int, const double*, double*, double*, double*, int32_t*, int32_t*,
-                          uint8_t*);
-
-template <int N>
-void launch_solve(hipStream_t s, const mpcqp_params& p, int B, const double* model, double* u0, double* X,
-                  double* U, int32_t* st, int32_t* it, uint8_t* ac) {
-  hipLaunchKernelGGL(k_solve<N>, dim3(B), dim3(kWave), 0, s, p, B, model, u0, X, U, st, it, ac);
+// ------------------------------------------------------------------ test hook: wave primitives
+// out[op][lane] for the 64-lane input `in` (tests/test_gpu_parity.py checks them with numpy).
+__global__ __launch_bounds__(kWave) void k_wave_ops(const double* __restrict__ in, double* __restrict__ out) {
+  const int lane = threadIdx.x;
+  const double v = in[lane];
+  const double a = fabs(v);
+  out[0 * kWave + lane] = scan_add(v, lane);
+  out[1 * kWave + lane] = rscan_add(v, lane);
+  out[2 * kWave + lane] = scan_max(a, lane);
+  out[3 * kWave + lane] = rscan_max(a, lane);
+  out[4 * kWave + lane] = wave_sum(v);
+  out[5 * kWave + lane] = wave_max(a);
+  out[6 * kWave + lane] = shr2(v);
+  out[7 * kWave + lane] = shl2(v);
+  out[8 * kWave + lane] = dpp<kWaveShr1>(v);
+  out[9 * kWave + lane] = readlane(v, 37);
 }
 
-typedef void (*launcher_t)(hipStream_t, const mpcqp_params&, int, const double*, double*, double*, double*,
-                           int32_t*, int32_t*, uint8_t*);
+// ------------------------------------------------------------------ dispatch
+struct Launch {
+  const mpcqp_params* p;
+  int B;
+  const double* model;
+  double* state;
+  double *u0, *X, *U;
+  int32_t *st, *it;
+  uint8_t* ac;
+};
+
+template <int N>
+void launch_solve(hipStream_t s, const Launch& L) {
+  hipLaunchKernelGGL(k_setup<N>, dim3(L.B), dim3(kWave), 0, s, *L.p, L.B, L.model, L.state);
+  if (L.p->method == MPCQP_METHOD_ADMM) hipLaunchKernelGGL(k_admm<N>, dim3(L.B), dim3(kWave), 0, s, *L.p, L.B, L.state);
+  hipLaunchKernelGGL(k_finish<N>, dim3(L.B), dim3(kWave), 0, s, *L.p, L.B, L.model, L.state, L.u0, L.X, L.U, L.st,
+                     L.it, L.ac);
+}
+
+typedef void (*launcher_t)(hipStream_t, const Launch&);
 
 #ifdef MPCQP_ONLY_N  // development builds: instantiate a single horizon
-#define MPCQP_L(N) ((N) == MPCQP_ONLY_N ? &launch_solve<((N) == MPCQP_ONLY_N ? (N) : MPCQP_ONLY_N)> : nullptr)
+#define MPCQP_L(N) ((N) == MPCQP_ONLY_N ? &launch_solve<MPCQP_ONLY_N> : nullptr)
 #else
 #define MPCQP_L(N) &launch_solve<N>
 #endif
 const launcher_t kLaunchers[MPCQP_MAX_HORIZON + 1] = {
-    nullptr,      MPCQP_L(1),  MPCQP_L(2),  MPCQP_L(3),  MPCQP_L(4),  MPCQP_L(5),  MPCQP_L(6),  MPCQP_L(7),
-    MPCQP_L(8),   MPCQP_L(9),  MPCQP_L(10), MPCQP_L(11), MPCQP_L(12), MPCQP_L(13), MPCQP_L(14), MPCQP_L(15),
-    MPCQP_L(16),  MPCQP_L(17), MPCQP_L(18), MPCQP_L(19), MPCQP_L(20), MPCQP_L(21), MPCQP_L(22), MPCQP_L(23),
-    MPCQP_L(24),  MPCQP_L(25), MPCQP_L(26), MPCQP_L(27), MPCQP_L(28), MPCQP_L(29), MPCQP_L(30), MPCQP_L(31)};
+    nullptr,     MPCQP_L(1),  MPCQP_L(2),  MPCQP_L(3),  MPCQP_L(4),  MPCQP_L(5),  MPCQP_L(6),  MPCQP_L(7),
+    MPCQP_L(8),  MPCQP_L(9),  MPCQP_L(10), MPCQP_L(11), MPCQP_L(12), MPCQP_L(13), MPCQP_L(14), MPCQP_L(15),
+    MPCQP_L(16), MPCQP_L(17), MPCQP_L(18), MPCQP_L(19), MPCQP_L(20), MPCQP_L(21), MPCQP_L(22), MPCQP_L(23),
+    MPCQP_L(24), MPCQP_L(25), MPCQP_L(26), MPCQP_L(27), MPCQP_L(28), MPCQP_L(29), MPCQP_L(30), MPCQP_L(31)};
 #undef MPCQP_L
 
 thread_local std::string g_err;
@@ -828,6 +1077,7 @@ int check_params(const mpcqp_params* p) {
   if (!p) return fail(MPCQP_E_ARG, "null params");
   if (p->horizon < 1 || p->horizon > MPCQP_MAX_HORIZON)
     return fail(MPCQP_E_HORIZON, "horizon " + std::to_string(p->horizon) + " outside [1, 31]");
+  if (!kLaunchers[p->horizon]) return fail(MPCQP_E_HORIZON, "horizon not compiled into this build");
   if (!(p->dt > 0.0) || !(p->wheelbase_px > 0.0)) return fail(MPCQP_E_ARG, "dt and wheelbase_px must be > 0");
   if (p->method != MPCQP_METHOD_ADMM && p->method != MPCQP_METHOD_NEWTON) return fail(MPCQP_E_ARG, "bad method");
   if (p->max_iter < 1 || p->check_termination < 1 || p->adaptive_rho_interval < 1 || p->polish_max_iter < 0 ||
@@ -846,6 +1096,7 @@ struct mpcqp_ws {
   int device;
   int built_B;
   double* model;
+  double* state;
 };
 
 extern "C" {
@@ -872,9 +1123,14 @@ int mpcqp_create(const mpcqp_params* p, int max_batch, int device, mpcqp_ws** ws
   w->max_batch = max_batch;
   w->device = device;
   w->built_B = -1;
-  const size_t bytes = sizeof(double) * (size_t)model_stride(p->horizon) * (size_t)max_batch;
-  e = hipMalloc(&w->model, bytes);
+  w->model = nullptr;
+  w->state = nullptr;
+  const size_t mbytes = sizeof(double) * (size_t)model_stride(p->horizon) * (size_t)max_batch;
+  const size_t sbytes = sizeof(double) * (size_t)state_stride(p->horizon) * (size_t)max_batch;
+  e = hipMalloc(&w->model, mbytes);
+  if (e == hipSuccess) e = hipMalloc(&w->state, sbytes);
   if (e != hipSuccess) {
+    if (w->model) (void)hipFree(w->model);
     delete w;
     return fail(MPCQP_E_HIP, std::string("hipMalloc: ") + hipGetErrorString(e));
   }
@@ -896,6 +1152,7 @@ void mpcqp_destroy(mpcqp_ws* ws) {
   if (!ws) return;
   (void)hipSetDevice(ws->device);
   (void)hipFree(ws->model);
+  (void)hipFree(ws->state);
   delete ws;
 }
 
@@ -917,12 +1174,25 @@ int mpcqp_solve(mpcqp_ws* ws, int B, double* u0, double* X, double* U, int32_t* 
   if (B != ws->built_B) return fail(MPCQP_E_STATE, "mpcqp_solve B differs from the last mpcqp_build");
   if (B == 0) return MPCQP_OK;
   hipStream_t s = static_cast<hipStream_t>(stream);
-  kLaunchers[ws->p.horizon](s, ws->p, B, ws->model, u0, X, U, status, iters, active);
+  Launch L{&ws->p, B, ws->model, ws->state, u0, X, U, status, iters, active};
+  kLaunchers[ws->p.horizon](s, L);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return fail(MPCQP_E_HIP, std::string("k_solve launch: ") + hipGetErrorString(e));
   return MPCQP_OK;
 }
 
 const double* mpcqp_model_buffer(const mpcqp_ws* ws) { return ws ? ws->model : nullptr; }
+
+const double* mpcqp_state_buffer(const mpcqp_ws* ws) { return ws ? ws->state : nullptr; }
+
+int mpcqp_state_stride(int horizon) { return state_stride(horizon); }
+
+int mpcqp_debug_wave_ops(const double* in, double* out, void* stream) {
+  if (!in || !out) return fail(MPCQP_E_ARG, "null argument");
+  hipLaunchKernelGGL(k_wave_ops, dim3(1), dim3(kWave), 0, static_cast<hipStream_t>(stream), in, out);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return fail(MPCQP_E_HIP, std::string("k_wave_ops launch: ") + hipGetErrorString(e));
+  return MPCQP_OK;
+}
 
 }  // extern "C"

@@ -126,6 +126,9 @@ _SYMBOLS = {
     "mpcqp_solve": ([ctypes.c_void_p, ctypes.c_int] + [ctypes.c_void_p] * 7, ctypes.c_int),
     "mpcqp_model_buffer": ([ctypes.c_void_p], ctypes.c_void_p),
     "mpcqp_model_stride": ([ctypes.c_int], ctypes.c_int),
+    "mpcqp_state_buffer": ([ctypes.c_void_p], ctypes.c_void_p),
+    "mpcqp_state_stride": ([ctypes.c_int], ctypes.c_int),
+    "mpcqp_debug_wave_ops": ([ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p], ctypes.c_int),
 }
 
 

@@ -1,0 +1,133 @@
+"""CPU tests of the oracle itself, pinned to the reference's golden vectors (tests/golden/).
+
+The oracle is the parity reference for the GPU path, so it is checked first:
+  * its vehicle model against the reference's f_discrete / linearize outputs,
+  * its QP against the reference's own known-answer test (tests/test_mpc_controller.py)
+    and against an independent solver (scipy trust-constr) on the un-condensed formulation,
+  * its closed loop against the reference TrajectoryTracker's own loop,
+  * the C restatement (CPU baseline) against the numpy exact solve.
+"""
+from __future__ import annotations
+
+import numpy as np
+import pytest
+
+import mpc_oracle as mo
+
+
+def test_vehicle_model_matches_reference_golden(golden):
+    g = golden("vehicle.npz")
+    for i in range(len(g["x"])):
+        fd = mo.f_discrete(g["x"][i], g["u"][i], g["dt"][i], g["L"][i])
+        A, B, fx = mo.linearize(g["x"][i], g["u"][i], g["dt"][i], g["L"][i])
+        np.testing.assert_array_equal(fd, g["f_discrete"][i])
+        np.testing.assert_array_equal(A, g["A"][i])
+        np.testing.assert_array_equal(B, g["B"][i])
+        np.testing.assert_array_equal(fx, g["fx"][i])
+
+
+def test_reference_known_answer_case():
+    """tests/test_mpc_controller.py:7-17 of the reference (MPCConfig(horizon=5), res 0.2)."""
+    p = mo.default_params(horizon=5, map_resolution=0.2)
+    x0 = np.array([0.0, 0.0, 0.0, 5.0])
+    ref = np.tile(np.array([1.0, 0.0, 0.0, 5.0]), (6, 1))
+    sol = mo.solve_exact(p, x0, ref)
+    assert sol.converged
+    assert sol.X[0, 1] > x0[0]  # the reference's assertion
+    np.testing.assert_allclose(sol.Umat[:, 0], [-9.1046224514, 0.0], atol=1e-9)
+    np.testing.assert_allclose(sol.X[0, 1], 0.5, atol=1e-12)
+
+
+def _random_case(rng, N):
+    plan_ref = np.column_stack([np.linspace(0, 30, N + 1), np.linspace(0, 5, N + 1),
+                                np.linspace(0.0, 0.8, N + 1), np.full(N + 1, 12.0)])
+    x0 = plan_ref[0] + rng.normal(0, 1, 4) * [2, 2, 0.3, 3]
+    return x0, plan_ref, rng.normal(0, 1, 2) * [3, 0.05]
+
+
+@pytest.mark.parametrize("seed", [0, 1])
+def test_condensed_solution_solves_full_formulation(seed):
+    """The condensed solution, lifted to the cvxpy variable vector (11N+5), is feasible for
+    the un-condensed QP of mpc_controller.py:53-117, attains the same objective, and agrees
+    with scipy's trust-constr on that formulation."""
+    from scipy.optimize import LinearConstraint, minimize
+
+    rng = np.random.default_rng(seed)
+    N = 5
+    p = mo.default_params(N)
+    x0, ref, up = _random_case(rng, N)
+    sol = mo.solve_exact(p, x0, ref, up)
+    P, q, r0, A, lo, hi, lay = mo.full_qp(p, x0, ref, up)
+    assert lay["n"] == 11 * N + 5 and A.shape[0] == 19 * N + 7
+    xs = mo.lift(p, sol, up)
+    z = A @ xs
+    assert np.all(z >= lo - 1e-9) and np.all(z <= hi + 1e-9)
+    np.testing.assert_allclose(0.5 * xs @ P @ xs + q @ xs + r0, sol.objective, rtol=1e-12)
+    res = minimize(lambda v: 0.5 * v @ P @ v + q @ v, np.zeros_like(xs), jac=lambda v: P @ v + q,
+                   hess=lambda v: P, method="trust-constr", constraints=[LinearConstraint(A, lo, hi)],
+                   options=dict(gtol=1e-12, xtol=1e-14, maxiter=6000))
+    assert np.abs(res.x[lay["oU"]: lay["oSv"]] - xs[lay["oU"]: lay["oSv"]]).max() < 1e-4
+    assert 0.5 * res.x @ P @ res.x + q @ res.x + r0 >= sol.objective - 1e-9
+
+
+def test_exact_solution_is_stationary():
+    rng = np.random.default_rng(5)
+    for N in (5, 10, 20):
+        p = mo.default_params(N)
+        x0, ref, up = _random_case(rng, N)
+        qp = mo.condense(p, x0, ref, up)
+        U, codes, its, ok = mo.solve_condensed(qp)
+        assert ok
+        assert np.abs(mo.gradient(qp, U)).max() <= 1e-9 * max(1.0, np.abs(qp.g).max())
+
+
+def test_closed_loop_matches_reference_loop(golden):
+    """The oracle's restatement of control_stage.py:84-150, driven by the exact solve,
+    reproduces the reference TrajectoryTracker's own loop (captured in closed_loop.npz)."""
+    plan = golden("default_plan.npz")
+    loop = golden("closed_loop.npz")
+    for N in (10, 15):
+        p = mo.default_params(N, float(plan["map_resolution"]))
+        rec: list = []
+        states = mo.track_loop(p, plan[f"ref_global_N{N}"], plan["start"], float(plan["yaw0"]), plan["goal"],
+                               100 if N == 10 else 300, record=rec)
+        ref_states = loop[f"N{N}_states"]
+        assert len(states) == len(ref_states) == 65
+        np.testing.assert_allclose(np.asarray(states), ref_states, rtol=0, atol=1e-9)
+        np.testing.assert_allclose(np.asarray([r[1] for r in rec]), loop[f"N{N}_window"], rtol=0, atol=1e-12)
+        np.testing.assert_allclose(np.asarray([r[2] for r in rec]), loop[f"N{N}_u_prev"], rtol=0, atol=1e-9)
+
+
+@pytest.mark.parametrize("cfg,B", [("config2", 4), ("config3", 96), ("config4", 48)])
+def test_c_restatement_matches_exact_oracle(cfg, B):
+    import cpu_solver
+    from mpcqp import scenarios
+
+    batch = getattr(scenarios, cfg)(B)
+    p = mo.default_params(batch.horizon)
+    for method in (0, 1):
+        out = cpu_solver.cpu_solve(p, batch.x0, batch.ref, batch.u_prev, method=method, nthreads=4)
+        assert (out["status"] == 1).all()
+        for b in range(B):
+            ex = mo.solve_exact(p, batch.x0[b], batch.ref[b], batch.u_prev[b])
+            err = np.abs(out["U"][b] - ex.Umat).max() / max(1.0, np.abs(ex.Umat).max())
+            assert err <= 1e-9, (b, err)
+            np.testing.assert_array_equal(out["active"][b], ex.active)
+
+
+def test_c_restatement_unwrap_is_numpy_bit_exact(golden):
+    """The C build step's np.unwrap against numpy on the golden edge cases (exact +-pi jumps)."""
+    import cpu_solver
+
+    g = golden("unwrap.npz")
+    p = mo.default_params(30)
+    for i, L in enumerate(g["lens"]):
+        N = int(L) - 1
+        pN = mo.default_params(N)
+        ref = np.zeros((1, N + 1, 4))
+        ref[0, :, 2] = g["p"][i, :L]
+        ref[0, :, 3] = 10.0
+        out = cpu_solver.cpu_solve(pN, np.zeros((1, 4)), ref, None, want_model=True)
+        yaw = out["model"][0, 7 * N + 2: 7 * N + 2 + 4 * (N + 1): 4]
+        np.testing.assert_array_equal(yaw, g["unwrapped"][i, :L])
+    assert p.horizon == 30
