@@ -156,6 +156,10 @@ int mpcqp_state_stride(int horizon);
  * reductions, lane shifts) to in[64] -> out[10 x 64] on the device. */
 int mpcqp_debug_wave_ops(const double* in, double* out, void* stream);
 
+/* Diagnostic builds only (-DMPCQP_STAMPS; the measured library returns MPCQP_E_ARG):
+ * per-phase s_memtime cycle sums over all waves since the last reset. */
+int mpcqp_debug_stamps(unsigned long long* out16, int reset);
+
 #ifdef __cplusplus
 }
 #endif

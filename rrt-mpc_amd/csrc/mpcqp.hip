@@ -152,6 +152,37 @@ __device__ __forceinline__ double shr2(double v) { return dpp<kWaveShr1>(dpp<kWa
 __device__ __forceinline__ double shl2(double v) { return dpp<kWaveShl1>(dpp<kWaveShl1>(v)); }
 __device__ __forceinline__ bool wave_any(bool b) { return __ballot(b) != 0ull; }
 
+// ------------------------------------------------------------------ diagnostic stamps
+// Built only with -DMPCQP_STAMPS (never in the measured library): per-phase s_memtime
+// cycle sums, flushed once per wave into g_stamps[] (read by mpcqp_debug_stamps).
+#ifdef MPCQP_STAMPS
+__device__ unsigned long long g_stamps[16];
+struct Stamps {
+  unsigned long long acc[6] = {0, 0, 0, 0, 0, 0};
+  unsigned long long t = 0;
+  __device__ __forceinline__ void begin() {
+    __builtin_amdgcn_sched_barrier(0);
+    t = __builtin_amdgcn_s_memtime();
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  __device__ __forceinline__ void end(int s) {
+    __builtin_amdgcn_sched_barrier(0);
+    acc[s] += __builtin_amdgcn_s_memtime() - t;
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  __device__ __forceinline__ void flush(int base) {
+    if (threadIdx.x == 0)
+      for (int s = 0; s < 6; ++s) atomicAdd(&g_stamps[base + s], acc[s]);
+  }
+};
+#else
+struct Stamps {
+  __device__ __forceinline__ void begin() {}
+  __device__ __forceinline__ void end(int) {}
+  __device__ __forceinline__ void flush(int) {}
+};
+#endif
+
 __device__ __forceinline__ double limit_scaling(double v) {
   return v < kMinScaling ? 1.0 : (v > kMaxScaling ? kMaxScaling : v);
 }
@@ -714,12 +745,19 @@ __global__ __launch_bounds__(kWave) void k_admm(mpcqp_params p, int B, double* _
   const double sg = p.sigma, alpha = p.alpha;
   bool bad = false, ok = false;
   int it = 0, nfact = 0;
+  Stamps T, T2;
+  T2.begin();
   while (it < p.max_iter && !bad && !ok) {
     {
       const double rw[3] = {rho, rho, rho};
+      T.begin();
       C.form(sg, rw);
+      T.end(0);
       ++nfact;
-      if (wave_any(!C.sweep())) {
+      T.begin();
+      const bool okf = C.sweep();
+      T.end(1);
+      if (wave_any(!okf)) {
         bad = true;
         break;
       }
@@ -735,6 +773,7 @@ __global__ __launch_bounds__(kWave) void k_admm(mpcqp_params p, int B, double* _
     while (!refactor && it < p.max_iter) {
       ++it;
       C.opaque();
+      T.begin();
       double tmp[3];
 #pragma unroll
       for (int r = 0; r < 3; ++r) tmp[r] = rho * z[r] - y[r];
@@ -755,7 +794,9 @@ __global__ __launch_bounds__(kWave) void k_admm(mpcqp_params p, int B, double* _
         y[r] = y[r] + rho * (v - zn);
         z[r] = zn;
       }
+      T.end(2);
       if (it % p.check_termination == 0 || it == p.max_iter) {
+        T.begin();
         double Ax[3];
         C.Cmul(x, Ax);
         const double Px = C.Pmul(x);
@@ -797,6 +838,7 @@ __global__ __launch_bounds__(kWave) void k_admm(mpcqp_params p, int B, double* _
         du *= ic;
         const double ep = p.eps_abs + p.eps_rel * fmax(nAx, nz);
         const double ed = p.eps_abs + p.eps_rel * fmax(fmax(nPx, nAty), nq) * ic;
+        T.end(3);
         if (!isfinite(pr) || !isfinite(du)) {
           bad = true;
           break;
@@ -833,6 +875,9 @@ __global__ __launch_bounds__(kWave) void k_admm(mpcqp_params p, int B, double* _
     sc[2] = (double)it;
     sc[3] = (double)nfact;
   }
+  T2.end(0);
+  T.flush(0);   // g_stamps[0..3]: form, sweep, ADMM iteration body, termination checks
+  T2.flush(4);  // g_stamps[4]: whole k_admm
 }
 
 // ------------------------------------------------------------------ K2c: polish + outputs
@@ -863,6 +908,8 @@ __global__ __launch_bounds__(kWave) void k_finish(mpcqp_params p, int B, const d
   const double x_admm = x;
   bool pol_ok = false;
   int pol_it = 0, n_ls = 0;
+  Stamps T, T2;
+  T2.begin();
 
   if (do_polish && !bad) {
     double zc[3];
@@ -879,12 +926,18 @@ __global__ __launch_bounds__(kWave) void k_finish(mpcqp_params p, int B, const d
         rw[r] = cd[r] ? 2.0 * C.wb[r] : 0.0;
         tmp[r] = cd[r] == 2 ? rw[r] * C.hi[r] : (cd[r] == 1 ? rw[r] * C.lo[r] : 0.0);
       }
+      T.begin();
       C.form(0.0, rw);
+      T.end(0);
       ++nfact;
-      if (wave_any(!C.sweep())) {
+      T.begin();
+      const bool okf = C.sweep();
+      T.end(1);
+      if (wave_any(!okf)) {
         bad = true;
         break;
       }
+      T.begin();
       const double rhs = C.CTmul(tmp) - C.qv;
       double xn = C.inv_mul(rhs);
       {  // one step of iterative refinement: res = rhs - M xn
@@ -903,12 +956,14 @@ __global__ __launch_bounds__(kWave) void k_finish(mpcqp_params p, int B, const d
         const int c2 = zn[r] > C.hi[r] ? 2 : (zn[r] < C.lo[r] ? 1 : 0);
         diff = diff || (c2 != cd[r]);
       }
+      T.end(2);
       if (!wave_any(diff)) {
         x = xn;
         pol_ok = true;
         break;
       }
       // Armijo backtracking on the scaled objective along d = xn - x
+      T.begin();
       const double dx = act ? xn - x : 0.0;
       const double Px = C.Pmul(x);
       const double Pd = C.Pmul(dx);
@@ -946,8 +1001,12 @@ __global__ __launch_bounds__(kWave) void k_finish(mpcqp_params p, int B, const d
       C.Cmul(x, zc);
 #pragma unroll
       for (int r = 0; r < 3; ++r) cd[r] = zc[r] > C.hi[r] ? 2 : (zc[r] < C.lo[r] ? 1 : 0);
+      T.end(3);
     }
   }
+  T2.end(0);
+  T.flush(8);   // g_stamps[8..11]: polish form, sweep, solve+check, line search
+  T2.flush(12); // g_stamps[12]: polish phase of k_finish
   int status;
   if (bad) {
     status = MPCQP_NUMERICAL_ERROR;
@@ -1186,6 +1245,23 @@ const double* mpcqp_model_buffer(const mpcqp_ws* ws) { return ws ? ws->model : n
 const double* mpcqp_state_buffer(const mpcqp_ws* ws) { return ws ? ws->state : nullptr; }
 
 int mpcqp_state_stride(int horizon) { return state_stride(horizon); }
+
+int mpcqp_debug_stamps(unsigned long long* out16, int reset) {
+#ifdef MPCQP_STAMPS
+  hipError_t e = hipDeviceSynchronize();
+  if (e == hipSuccess && out16) e = hipMemcpyFromSymbol(out16, HIP_SYMBOL(g_stamps), sizeof(unsigned long long) * 16);
+  if (e == hipSuccess && reset) {
+    unsigned long long z[16] = {0};
+    e = hipMemcpyToSymbol(HIP_SYMBOL(g_stamps), z, sizeof(z));
+  }
+  if (e != hipSuccess) return fail(MPCQP_E_HIP, std::string("stamps: ") + hipGetErrorString(e));
+  return MPCQP_OK;
+#else
+  (void)out16;
+  (void)reset;
+  return fail(MPCQP_E_ARG, "not a -DMPCQP_STAMPS diagnostic build");
+#endif
+}
 
 int mpcqp_debug_wave_ops(const double* in, double* out, void* stream) {
   if (!in || !out) return fail(MPCQP_E_ARG, "null argument");

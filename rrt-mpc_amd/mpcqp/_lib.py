@@ -129,6 +129,7 @@ _SYMBOLS = {
     "mpcqp_state_buffer": ([ctypes.c_void_p], ctypes.c_void_p),
     "mpcqp_state_stride": ([ctypes.c_int], ctypes.c_int),
     "mpcqp_debug_wave_ops": ([ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p], ctypes.c_int),
+    "mpcqp_debug_stamps": ([ctypes.c_void_p, ctypes.c_int], ctypes.c_int),
 }
 
 

@@ -1,0 +1,105 @@
+"""GPU tests of the reference-facing surface: MPCController.solve (B=1 shim),
+TrajectoryTracker.step / track, against the reference's own known answer and closed loop."""
+from __future__ import annotations
+
+import logging
+from types import SimpleNamespace
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def test_mpc_controller_reference_test_case(cuda):
+    """Reference tests/test_mpc_controller.py:7-17, plus the exact optimum."""
+    from mpcqp.config import MPCConfig
+    from mpcqp.control.mpc_controller import MPCController
+
+    cfg = MPCConfig(horizon=5)
+    controller = MPCController(cfg.to_parameters(map_resolution=0.2))
+    x0 = np.array([0.0, 0.0, 0.0, 5.0])
+    ref = np.tile(np.array([1.0, 0.0, 0.0, 5.0]), (cfg.horizon + 1, 1))
+    u0, Xp, Up = controller.solve(x0, ref)
+    assert u0 is not None and Xp is not None and Up is not None
+    assert Xp[0, 1] > x0[0]
+    assert u0.shape == (2,) and Xp.shape == (4, 6) and Up.shape == (2, 5)
+    np.testing.assert_allclose(u0, [-9.1046224514, 0.0], atol=1e-8)
+    np.testing.assert_allclose(Xp[:, 0], x0)
+
+
+def _default_plan(golden):
+    g = golden("default_plan.npz")
+    planning = SimpleNamespace(plan=SimpleNamespace(success=True, path=[tuple(map(float, p)) for p in g["path"]]))
+    maps = SimpleNamespace(start=tuple(g["start"]), goal=tuple(g["goal"]))
+    return g, planning, maps
+
+
+@pytest.mark.parametrize("N,sim_steps", [(10, 100), (15, 300)])
+def test_tracker_reproduces_reference_closed_loop(cuda, golden, N, sim_steps):
+    """BASELINE config 1 (N=10, 100 steps) and the code default (N=15): the reference's
+    TrajectoryTracker loop (closed_loop.npz, exact solve substituted for OSQP) is reproduced
+    step for step with every QP solved on the GPU."""
+    from mpcqp.config import MPCConfig, VizConfig
+    from mpcqp.pipeline.control_stage import TrajectoryTracker
+
+    g, planning, maps = _default_plan(golden)
+    loop = golden("closed_loop.npz")
+    tracker = TrajectoryTracker(MPCConfig(horizon=N, sim_steps=sim_steps), VizConfig())
+    result = tracker.track(planning, maps, map_resolution=float(g["map_resolution"]), visualize=False)
+    states = np.asarray(result.states)
+    ref_states = loop[f"N{N}_states"]
+    assert states.shape == ref_states.shape == (65, 4)
+    np.testing.assert_allclose(states, ref_states, rtol=0, atol=1e-7)
+    assert np.hypot(*(states[-1, :2] - np.asarray(maps.goal))) < 8.0
+
+
+def test_step_is_one_loop_iteration(cuda, golden):
+    from mpcqp.config import MPCConfig, VizConfig
+    from mpcqp.pipeline.control_stage import TrajectoryTracker
+
+    loop = golden("closed_loop.npz")
+    tracker = TrajectoryTracker(MPCConfig(horizon=15), VizConfig())
+    params = tracker.mpc.to_parameters(0.8)
+    for k in (0, 10, 40):
+        nxt, u0, Xp = tracker.step(loop["N15_x0"][k], loop["N15_window"][k], loop["N15_u_prev"][k], params)
+        np.testing.assert_allclose(u0, loop["N15_u0"][k], rtol=0, atol=1e-8)
+        np.testing.assert_allclose(nxt, loop["N15_states"][k], rtol=0, atol=1e-8)
+        assert Xp.shape == (4, 16)
+
+
+def test_unsolvable_input_takes_the_relaxation_path_and_aborts(cuda, caplog):
+    """Non-finite data -> status numerical_error -> relaxation retry (control_stage.py:45-56)
+    -> still None -> (None, None, None), as the reference's loop expects (:108-110)."""
+    from mpcqp.config import MPCConfig, VizConfig
+    from mpcqp.pipeline.control_stage import TrajectoryTracker
+
+    tracker = TrajectoryTracker(MPCConfig(horizon=5), VizConfig())
+    params = tracker.mpc.to_parameters(0.8)
+    state = np.array([np.nan, 0.0, 0.0, 5.0])
+    ref = np.tile(np.array([1.0, 0.0, 0.0, 5.0]), (6, 1))
+    with caplog.at_level(logging.WARNING):
+        out = tracker.step(state, ref, np.zeros(2), params)
+    assert out == (None, None, None)
+    assert any("relaxation" in r.getMessage() for r in caplog.records)
+
+
+def test_batched_controller_reuses_device_inputs(cuda):
+    """Device-resident inputs are consumed in place (no host round trip) and results stay on
+    the device."""
+    import torch
+    from mpcqp import scenarios
+    from mpcqp.config import MPCConfig
+    from mpcqp.control.mpc_controller import BatchedMPCController
+
+    b = scenarios.config3(128)
+    ctrl = BatchedMPCController(MPCConfig(horizon=20).to_parameters(0.8), 128, device="cuda:0")
+    x0 = torch.from_numpy(b.x0).to(cuda)
+    ref = torch.from_numpy(b.ref).to(cuda)
+    up = torch.from_numpy(b.u_prev).to(cuda)
+    sol = ctrl.solve_batch(x0, ref, up)
+    assert sol.u0.device.type == "cuda" and sol.X.shape == (128, 4, 21)
+    torch.cuda.synchronize()
+    assert (sol.status == 1).all().item()
+    np.testing.assert_array_equal(sol.u0.cpu().numpy(), sol.U[:, :, 0].cpu().numpy())
+    ctrl.close()
