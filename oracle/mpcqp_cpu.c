@@ -478,6 +478,14 @@ void mpcqp_cpu_solve_one(const mpcqp_params* p, const double* model, double* u0,
   for (int i = 0; i < n; ++i) x[i] = 0.0;
   for (int r = 0; r < m; ++r) z[r] = y[r] = 0.0;
   int admm_ok = 0, bad = 0;
+  /* non-finite problem data (NaN/inf in x0, ref, u_prev) -> numerical error, as k_setup */
+  for (int i = 0; i < n && !bad; ++i) {
+    if (!isfinite(s->q[i])) bad = 1;
+    for (int j = 0; j < n; ++j)
+      if (!isfinite(s->P[i][j])) bad = 1;
+  }
+  for (int r = 0; r < m && !bad; ++r)
+    if (!isfinite(s->l[r]) || !isfinite(s->u[r])) bad = 1;
 
   if (p->method == MPCQP_METHOD_ADMM) {
     double rho = p->rho;
@@ -539,7 +547,10 @@ void mpcqp_cpu_solve_one(const mpcqp_params* p, const double* model, double* u0,
         du *= ic;
         const double ep = p->eps_abs + p->eps_rel * fmax(nAx, nz);
         const double ed = p->eps_abs + p->eps_rel * fmax(fmax(nPx, nAty), nq) * ic;
-        if (!isfinite(pr) || !isfinite(du)) {
+        int nonfinite = 0; /* fmax drops NaNs: test the iterate itself */
+        for (int i = 0; i < n; ++i) nonfinite |= !isfinite(x[i]);
+        for (int r = 0; r < m; ++r) nonfinite |= !isfinite(z[r]) || !isfinite(y[r]);
+        if (nonfinite || !isfinite(pr) || !isfinite(du)) {
           bad = 1;
           break;
         }
@@ -600,6 +611,12 @@ void mpcqp_cpu_solve_one(const mpcqp_params* p, const double* model, double* u0,
       double zn[MAXR];
       Cmul(s, xn, zn);
       codes_of(s, zn, cn);
+      int nonfinite = 0;
+      for (int i = 0; i < n; ++i) nonfinite |= !isfinite(xn[i]);
+      if (nonfinite) {
+        bad = 1;
+        break;
+      }
       if (memcmp(cn, cd, m) == 0) {
         memcpy(x, xn, sizeof(double) * n);
         pol_ok = 1;
@@ -645,6 +662,7 @@ void mpcqp_cpu_solve_one(const mpcqp_params* p, const double* model, double* u0,
     } else
       st = MPCQP_MAX_ITER_REACHED;
   }
+  for (int i = 0; i < n; ++i) bad |= !isfinite(x[i]);
   if (bad) st = MPCQP_NUMERICAL_ERROR;
 
   /* ---- outputs (unscaled) ---- */

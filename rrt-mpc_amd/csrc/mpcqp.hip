@@ -152,6 +152,11 @@ __device__ __forceinline__ double shr2(double v) { return dpp<kWaveShr1>(dpp<kWa
 __device__ __forceinline__ double shl2(double v) { return dpp<kWaveShl1>(dpp<kWaveShl1>(v)); }
 __device__ __forceinline__ bool wave_any(bool b) { return __ballot(b) != 0ull; }
 
+// Every kernel runs one wavefront per workgroup, and the LDS operations of one wavefront
+// execute in program order: a broadcast through LDS needs only a compiler-level ordering
+// point (wavefront-scope fence), not an s_barrier with its lgkmcnt(0) drain.
+__device__ __forceinline__ void lds_sync() { __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront"); }
+
 // ------------------------------------------------------------------ diagnostic stamps
 // Built only with -DMPCQP_STAMPS (never in the measured library): per-phase s_memtime
 // cycle sums, flushed once per wave into g_stamps[] (read by mpcqp_debug_stamps).
@@ -498,9 +503,14 @@ __global__ __launch_bounds__(kWave) void k_setup(mpcqp_params p, int B, const do
 
   // ---- write the solver state ----
   double* st = state + (size_t)b * state_stride(N);
+  bool finite = isfinite(qv) && isfinite(cscale);
   if (act) {
     // symmetric Pbar: the lower-triangle value (computed by column `min`) for both halves
-    for (int i = 0; i < n; ++i) st[i * n + lane] = i >= lane ? sm.P[i * LD + lane] : sm.P[lane * LD + i];
+    for (int i = 0; i < n; ++i) {
+      const double v = i >= lane ? sm.P[i * LD + lane] : sm.P[lane * LD + i];
+      finite = finite && isfinite(v);
+      st[i * n + lane] = v;
+    }
   }
   double* lf = st + state_lane_off(N);
   double wb[3];
@@ -509,7 +519,10 @@ __global__ __launch_bounds__(kWave) void k_setup(mpcqp_params p, int B, const do
     lo[r] *= E[r];
     hi[r] *= E[r];
     wb[r] = E[r] > 0.0 ? cscale * wt[r] / (E[r] * E[r]) : 0.0;
+    finite = finite && isfinite(lo[r]) && isfinite(hi[r]);
   }
+  // non-finite data (NaN/inf in x0, ref or u_prev) -> status MPCQP_NUMERICAL_ERROR
+  const bool bad_input = wave_any(!finite);
   lf[kFq * kWave + lane] = qv;
   lf[kFD * kWave + lane] = D;
   lf[kFx * kWave + lane] = 0.0;
@@ -523,9 +536,9 @@ __global__ __launch_bounds__(kWave) void k_setup(mpcqp_params p, int B, const do
   if (lane == 0) {
     double* sc = st + state_scal_off(N);
     sc[0] = cscale;
-    sc[1] = 0.0;  // admm_ok
-    sc[2] = 0.0;  // admm iterations
-    sc[3] = 0.0;  // factorizations
+    sc[1] = bad_input ? -1.0 : 0.0;  // ADMM flag: -1 numerical error, 0 not converged, 1 converged
+    sc[2] = 0.0;                     // admm iterations
+    sc[3] = 0.0;                     // factorizations
   }
 }
 
@@ -548,7 +561,8 @@ struct Ctx {
   double r[n];
   double sig;
 
-  __device__ __forceinline__ void load(const double* st, int ln, double dt_, double* buf_, double* sv_, double* Dl_) {
+  __device__ __forceinline__ void load(const double* st, int ln, double dt_, double* buf_, double* sv_, double* Dl_,
+                                       double* Ps) {
     lane = ln;
     act = ln < n;
     even = act && ((ln & 1) == 0);
@@ -556,7 +570,9 @@ struct Ctx {
     buf = buf_;
     sv = sv_;
     Dl = Dl_;
-    P = st;
+    // Pbar is re-read by every factorization and every P-product: stage it in LDS once
+    for (int i = ln; i < n * n; i += kWave) Ps[i] = st[i];
+    P = Ps;
     const double* lf = st + state_lane_off(N);
     qv = lf[kFq * kWave + ln];
     D = lf[kFD * kWave + ln];
@@ -603,9 +619,9 @@ struct Ctx {
   }
   // broadcast v (one value per lane) through LDS
   __device__ __forceinline__ void put(double v) const {
-    __syncthreads();
+    lds_sync();
     buf[lane] = act ? v : 0.0;
-    __syncthreads();
+    lds_sync();
   }
   // (Pbar v)_lane, Pbar symmetric: column reads are coalesced
   __device__ __forceinline__ double Pmul(double v) const {
@@ -640,9 +656,9 @@ struct Ctx {
     const double suf = rscan_add(even ? ev : 0.0, lane);  // sum over v rows >= lane/2
     const double du2 = E[2] * E[2] * rw[2];
     const double du2n = shl2(du2);
-    __syncthreads();
+    lds_sync();
     if (even) sv[lane >> 1] = suf;
-    __syncthreads();
+    lds_sync();
     double diag = E[1] * E[1] * rw[1] + du2;
     if (ln + 2 < n) diag += du2n;
     const int col = ln < n ? ln : 0;
@@ -665,21 +681,16 @@ struct Ctx {
   // Symmetric sweep operator on the rows in r[]: afterwards A^{-1} = -sig * r (row `lane`).
   // The pivot row of step k is a scalar multiple of its own row (symmetry), so it is carried
   // in `sig` and every step is n uniform FMAs (no per-element select for the pivot lane).
-  // The pivot loop is unrolled at compile time (sweep_step<K>) so every register index is
-  // static and the row is updated in place.  false on a non-positive pivot.
-  // Symmetric sweep operator on the rows in r[]: afterwards A^{-1} = -sig * r (row `lane`).
-  // The pivot row of step k is a scalar multiple of its own row (symmetry), so it is carried
-  // in `sig` and every step is n uniform FMAs (no per-element select for the pivot lane).
   // The row rotates one slot per step, so the pivot slot is always r[0] and the pivot loop
   // stays rolled (static register indices).  false on a non-positive pivot.
   __device__ __forceinline__ bool sweep() {
     bool ok = true;
     for (int k = 0; k < n; ++k) {
-      __syncthreads();
+      lds_sync();
       const double colk = sig * r[0];
       buf[lane] = colk;
       if (lane < n) buf[lane + n] = colk;  // wrapped copy: buf[i + n] == buf[i]
-      __syncthreads();
+      lds_sync();
       const double d = buf[k];
       ok = ok && (d > 0.0) && isfinite(d);
       const double inv = 1.0 / d;
@@ -725,6 +736,7 @@ struct Ctx {
 
 template <int N>
 struct SolveSmem {
+  double P[4 * N * N];  // Pbar, row-major n x n (column reads by lane are conflict-free)
   double buf[2 * kWave];
   double sv[N + 1];
   double Dl[2 * N];
@@ -738,12 +750,13 @@ __global__ __launch_bounds__(kWave) void k_admm(mpcqp_params p, int B, double* _
   if (b >= B) return;
   double* st = state + (size_t)b * state_stride(N);
   Ctx<N> C;
-  C.load(st, threadIdx.x, p.dt, sm.buf, sm.sv, sm.Dl);
+  C.load(st, threadIdx.x, p.dt, sm.buf, sm.sv, sm.Dl, sm.P);
   const bool act = C.act;
   double x = 0.0, z[3] = {0.0, 0.0, 0.0}, y[3] = {0.0, 0.0, 0.0};
   double rho = p.rho;
   const double sg = p.sigma, alpha = p.alpha;
-  bool bad = false, ok = false;
+  bool bad = st[state_scal_off(N) + 1] < 0.0;  // non-finite problem data (k_setup)
+  bool ok = false;
   int it = 0, nfact = 0;
   Stamps T, T2;
   T2.begin();
@@ -839,7 +852,9 @@ __global__ __launch_bounds__(kWave) void k_admm(mpcqp_params p, int B, double* _
         const double ep = p.eps_abs + p.eps_rel * fmax(nAx, nz);
         const double ed = p.eps_abs + p.eps_rel * fmax(fmax(nPx, nAty), nq) * ic;
         T.end(3);
-        if (!isfinite(pr) || !isfinite(du)) {
+        // fmax drops NaNs, so test the iterate itself
+        if (wave_any(!isfinite(x) || !isfinite(z[0] + z[1] + z[2]) || !isfinite(y[0] + y[1] + y[2])) ||
+            !isfinite(pr) || !isfinite(du)) {
           bad = true;
           break;
         }
@@ -894,12 +909,12 @@ __global__ __launch_bounds__(kWave) void k_finish(mpcqp_params p, int B, const d
   const int lane = threadIdx.x;
   const double* st = state + (size_t)b * state_stride(N);
   Ctx<N> C;
-  C.load(st, lane, p.dt, sm.buf, sm.sv, sm.Dl);
+  C.load(st, lane, p.dt, sm.buf, sm.sv, sm.Dl, sm.P);
   const bool act = C.act;
   const bool use_admm = p.method == MPCQP_METHOD_ADMM;
   const bool do_polish = !use_admm || p.polish != 0;
   const double* sc = st + state_scal_off(N);
-  const double admm_flag = use_admm ? sc[1] : 0.0;
+  const double admm_flag = sc[1];  // -1: non-finite data (k_setup) or ADMM numerical error
   bool bad = admm_flag < 0.0;
   const bool admm_ok = admm_flag > 0.0;
   const int admm_it = use_admm ? (int)sc[2] : 0;
@@ -957,6 +972,10 @@ __global__ __launch_bounds__(kWave) void k_finish(mpcqp_params p, int B, const d
         diff = diff || (c2 != cd[r]);
       }
       T.end(2);
+      if (wave_any(!isfinite(xn))) {
+        bad = true;
+        break;
+      }
       if (!wave_any(diff)) {
         x = xn;
         pol_ok = true;
@@ -1007,6 +1026,7 @@ __global__ __launch_bounds__(kWave) void k_finish(mpcqp_params p, int B, const d
   T2.end(0);
   T.flush(8);   // g_stamps[8..11]: polish form, sweep, solve+check, line search
   T2.flush(12); // g_stamps[12]: polish phase of k_finish
+  if (wave_any(!isfinite(x))) bad = true;
   int status;
   if (bad) {
     status = MPCQP_NUMERICAL_ERROR;
