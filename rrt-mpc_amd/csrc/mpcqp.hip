@@ -21,6 +21,7 @@
 #include <cstring>
 #include <new>
 #include <string>
+#include <type_traits>
 #include <utility>
 
 #include "../../include/mpcqp.h"
@@ -35,7 +36,6 @@ constexpr double kMaxScaling = 1e4;
 constexpr double kRhoMin = 1e-6;
 constexpr double kRhoMax = 1e6;
 constexpr double kDivTol = 1e-30;
-constexpr int kChunk = 8;  // broadcast operands kept in flight per dot-product chunk
 
 // ------------------------------------------------------------------ layouts
 __host__ __device__ constexpr int model_stride(int N) { return ((11 * N + 10) + 7) / 8 * 8; }
@@ -151,6 +151,50 @@ __device__ __forceinline__ double wave_max(double v) {  // v >= 0
 __device__ __forceinline__ double shr2(double v) { return dpp<kWaveShr1>(dpp<kWaveShr1>(v)); }
 __device__ __forceinline__ double shl2(double v) { return dpp<kWaveShl1>(dpp<kWaveShl1>(v)); }
 __device__ __forceinline__ bool wave_any(bool b) { return __ballot(b) != 0ull; }
+
+// ---- register broadcasts for the dense row-per-lane products (no LDS)
+// A dense product over a vector v distributed one element per lane needs every lane to see
+// every v_j.  bcast() replicates each 16-lane row of v into all four rows with the gfx950
+// permlane swaps (w[c] lane l = v[16c + (l & 15)]); v_fmac_f64 with DPP row_newbcast:L then
+// reads lane L of each row's copy as its multiplicand, so a broadcast-FMA is ONE VALU
+// instruction with no memory latency.  Must run with all 64 lanes active.
+template <int NW>  // rows needed: ceil(n / 16)
+__device__ __forceinline__ void bcast(double v, double w[4]) {
+  const int lo = __double2loint(v), hi = __double2hiint(v);
+  const auto l16 = __builtin_amdgcn_permlane16_swap(lo, lo, false, false);  // rows {0,0,2,2} / {1,1,3,3}
+  const auto h16 = __builtin_amdgcn_permlane16_swap(hi, hi, false, false);
+  const auto la = __builtin_amdgcn_permlane32_swap(l16[0], l16[0], false, false);  // row 0 x4 / row 2 x4
+  const auto ha = __builtin_amdgcn_permlane32_swap(h16[0], h16[0], false, false);
+  w[0] = __hiloint2double(ha[0], la[0]);
+  if constexpr (NW > 1) {
+    const auto lb = __builtin_amdgcn_permlane32_swap(l16[1], l16[1], false, false);  // row 1 x4 / row 3 x4
+    const auto hb = __builtin_amdgcn_permlane32_swap(h16[1], h16[1], false, false);
+    w[1] = __hiloint2double(hb[0], lb[0]);
+    if constexpr (NW > 3) w[3] = __hiloint2double(hb[1], lb[1]);
+  }
+  if constexpr (NW > 2) w[2] = __hiloint2double(ha[1], la[1]);
+  // DPP reads of a VGPR need two wait states after its VALU write; tie the pad to w
+  if constexpr (NW == 1) asm volatile("s_nop 1" : "+v"(w[0]));
+  if constexpr (NW == 2) asm volatile("s_nop 1" : "+v"(w[0]), "+v"(w[1]));
+  if constexpr (NW == 3) asm volatile("s_nop 1" : "+v"(w[0]), "+v"(w[1]), "+v"(w[2]));
+  if constexpr (NW == 4) asm volatile("s_nop 1" : "+v"(w[0]), "+v"(w[1]), "+v"(w[2]), "+v"(w[3]));
+}
+// acc += w[lane 16*row + L] * m   (one v_fmac_f64_dpp)
+template <int L>
+__device__ __forceinline__ void fmac_bc(double& acc, double w, double m) {
+  asm("v_fmac_f64_dpp %0, %1, %2 row_newbcast:%3 row_mask:0xf bank_mask:0xf" : "+v"(acc) : "v"(w), "v"(m), "i"(L));
+}
+// compile-time loop: f(std::integral_constant<int, I>) for I in [B, E)
+template <int B, int E>
+struct Unroll {
+  template <class F>
+  __device__ __forceinline__ static void run(F&& f) {
+    if constexpr (B < E) {
+      f(std::integral_constant<int, B>{});
+      Unroll<B + 1, E>::run(f);
+    }
+  }
+};
 
 // Every kernel runs one wavefront per workgroup, and the LDS operations of one wavefront
 // execute in program order: a broadcast through LDS needs only a compiler-level ordering
@@ -557,9 +601,9 @@ struct Ctx {
   double* buf;                   // LDS broadcast buffer, >= 2*kWave doubles
   double* sv;                    // LDS, N+1 doubles
   double* Dl;                    // LDS copy of D (n doubles)
-  // KKT inverse, row `lane`: A^{-1}[lane][j] = -sig * r[j] (symmetric sweep operator, row scale sig)
+  static constexpr int kNW = (n + 15) / 16;  // 16-lane rows holding the n variables
+  // KKT inverse, row `lane`: A^{-1}[lane][j] = -r[j] (symmetric sweep operator)
   double r[n];
-  double sig;
 
   __device__ __forceinline__ void load(const double* st, int ln, double dt_, double* buf_, double* sv_, double* Dl_,
                                        double* Ps) {
@@ -617,36 +661,19 @@ struct Ctx {
     if (lane + 2 < n) t -= n2;
     return act ? D * t : 0.0;
   }
-  // broadcast v (one value per lane) through LDS
-  __device__ __forceinline__ void put(double v) const {
-    lds_sync();
-    buf[lane] = act ? v : 0.0;
-    lds_sync();
-  }
-  // (Pbar v)_lane, Pbar symmetric: column reads are coalesced
+  // (Pbar v)_lane, Pbar symmetric: lane reads its row as a conflict-free column of the LDS copy
   __device__ __forceinline__ double Pmul(double v) const {
-    put(v);
+    double w[4];
+    bcast<kNW>(act ? v : 0.0, w);
     const int col = act ? lane : 0;
-    double acc0 = 0.0, acc1 = 0.0;
-#pragma unroll
-    for (int j0 = 0; j0 < n; j0 += kChunk) {
-      double pv[kChunk], bv[kChunk];
-#pragma unroll
-      for (int t = 0; t < kChunk; ++t)
-        if (j0 + t < n) {
-          pv[t] = P[(j0 + t) * n + col];
-          bv[t] = buf[j0 + t];
-        }
-#pragma unroll
-      for (int t = 0; t < kChunk; t += 2) {
-        if (j0 + t < n) acc0 = fma(pv[t], bv[t], acc0);
-        if (j0 + t + 1 < n) acc1 = fma(pv[t + 1], bv[t + 1], acc1);
-      }
-      __builtin_amdgcn_sched_barrier(0);
-    }
-    return act ? acc0 + acc1 : 0.0;
+    double a[4] = {0.0, 0.0, 0.0, 0.0};
+    Unroll<0, n>::run([&](auto jc) {
+      constexpr int j = decltype(jc)::value;
+      fmac_bc<j % 16>(a[j % 4], w[j / 16], P[j * n + col]);
+    });
+    return act ? (a[0] + a[1]) + (a[2] + a[3]) : 0.0;
   }
-  // KKT matrix A = Pbar + s I + Cbar' diag(rw) Cbar, row `lane` -> r[] (sig = 1)
+  // KKT matrix A = Pbar + s I + Cbar' diag(rw) Cbar, row `lane` -> r[]
   __device__ __forceinline__ void form(double s, const double rw[3]) {
     // opaque lane copy: keeps per-column masks/addresses from being hoisted out of solver loops
     int ln = lane;
@@ -662,8 +689,11 @@ struct Ctx {
     double diag = E[1] * E[1] * rw[1] + du2;
     if (ln + 2 < n) diag += du2n;
     const int col = ln < n ? ln : 0;
-#pragma unroll
-    for (int j = 0; j < n; ++j) {
+    const double Dm = ln < n ? D : 0.0;
+    double wD[4];
+    bcast<kNW>(Dm, wD);  // D_j of every lane j
+    Unroll<0, n>::run([&](auto jc) {
+      constexpr int j = decltype(jc)::value;
       double t = 0.0;
       if ((j & 1) == 0 && ev_ln) {
         const int mx = (ln > j ? ln : j) >> 1;
@@ -672,65 +702,50 @@ struct Ctx {
       if (j == ln) t += diag;
       if (j == ln + 2) t -= du2n;
       if (j + 2 == ln) t -= du2;
-      const double v = P[j * n + col] + D * Dl[j] * t + (j == ln ? s : 0.0);
-      r[j] = ln < n ? v : 0.0;
-      if ((j % kChunk) == kChunk - 1) __builtin_amdgcn_sched_barrier(0);
-    }
-    sig = 1.0;
+      double v = ln < n ? P[j * n + col] + (j == ln ? s : 0.0) : 0.0;
+      fmac_bc<j % 16>(v, wD[j / 16], Dm * t);
+      r[j] = v;
+    });
   }
-  // Symmetric sweep operator on the rows in r[]: afterwards A^{-1} = -sig * r (row `lane`).
-  // The pivot row of step k is a scalar multiple of its own row (symmetry), so it is carried
-  // in `sig` and every step is n uniform FMAs (no per-element select for the pivot lane).
-  // The row rotates one slot per step, so the pivot slot is always r[0] and the pivot loop
-  // stays rolled (static register indices).  false on a non-positive pivot.
+  // Symmetric sweep operator on the rows in r[]: afterwards A^{-1} = -r (row `lane`).
+  // Step k: every lane needs its own A[i][k] (register r[k]) and the pivot row A[k][j] =
+  // A[j][k] (symmetry) -- the column r[k] of all lanes, register-broadcast by bcast() and read
+  // through DPP row_newbcast, so each update r[j] += coef * A[k][j] is one v_fmac_f64_dpp.
+  // The pivot row itself is the same FMA with coef = 1/d - 1 (A[k][j] <- A[k][j] / d), so the
+  // update is uniform over lanes.  The step loop is unrolled at compile time (static register
+  // indices and DPP lane immediates).  false on a non-positive pivot.
   __device__ __forceinline__ bool sweep() {
     bool ok = true;
-    for (int k = 0; k < n; ++k) {
-      lds_sync();
-      const double colk = sig * r[0];
-      buf[lane] = colk;
-      if (lane < n) buf[lane + n] = colk;  // wrapped copy: buf[i + n] == buf[i]
-      lds_sync();
-      const double d = buf[k];
+    Unroll<0, n>::run([&](auto kc) {
+      constexpr int k = decltype(kc)::value;
+      double w[4];
+      bcast<kNW>(r[k], w);
+      const double d = readlane(r[k], k);
       ok = ok && (d > 0.0) && isfinite(d);
       const double inv = 1.0 / d;
       const bool piv = lane == k;
-      const double c = piv ? 0.0 : r[0] * inv;
-      const double* colv = buf + k;
-#pragma unroll
-      for (int j0 = 1; j0 < n; j0 += kChunk) {
-        double bv[kChunk];
-#pragma unroll
-        for (int t = 0; t < kChunk; ++t)
-          if (j0 + t < n) bv[t] = colv[j0 + t];
-#pragma unroll
-        for (int t = 0; t < kChunk; ++t)
-          if (j0 + t < n) r[j0 + t - 1] = fma(-c, bv[t], r[j0 + t]);
-        __builtin_amdgcn_sched_barrier(0);
-      }
-      r[n - 1] = piv ? -1.0 / sig : c;
-      sig = piv ? sig * inv : sig;
-    }
+      const double ck = r[k] * inv;
+      const double coef = piv ? inv - 1.0 : -ck;
+      // next pivot column first: the next step's broadcast depends only on it
+      if constexpr (k + 1 < n) fmac_bc<(k + 1) % 16>(r[k + 1], w[(k + 1) / 16], coef);
+      Unroll<0, n>::run([&](auto jc) {
+        constexpr int j = decltype(jc)::value;
+        if constexpr (j != k && j != k + 1) fmac_bc<j % 16>(r[j], w[j / 16], coef);
+      });
+      r[k] = piv ? -inv : ck;
+    });
     return ok;
   }
   // (A^{-1} v)_lane
   __device__ __forceinline__ double inv_mul(double v) const {
-    put(v);
-    double acc0 = 0.0, acc1 = 0.0;
-#pragma unroll
-    for (int j0 = 0; j0 < n; j0 += kChunk) {
-      double bv[kChunk];
-#pragma unroll
-      for (int t = 0; t < kChunk; ++t)
-        if (j0 + t < n) bv[t] = buf[j0 + t];
-#pragma unroll
-      for (int t = 0; t < kChunk; t += 2) {
-        if (j0 + t < n) acc0 = fma(r[j0 + t], bv[t], acc0);
-        if (j0 + t + 1 < n) acc1 = fma(r[j0 + t + 1], bv[t + 1], acc1);
-      }
-      __builtin_amdgcn_sched_barrier(0);
-    }
-    return act ? -sig * (acc0 + acc1) : 0.0;
+    double w[4];
+    bcast<kNW>(act ? v : 0.0, w);
+    double a[4] = {0.0, 0.0, 0.0, 0.0};
+    Unroll<0, n>::run([&](auto jc) {
+      constexpr int j = decltype(jc)::value;
+      fmac_bc<j % 16>(a[j % 4], w[j / 16], r[j]);
+    });
+    return act ? -((a[0] + a[1]) + (a[2] + a[3])) : 0.0;
   }
 };
 
