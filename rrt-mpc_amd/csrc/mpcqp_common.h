@@ -1,0 +1,258 @@
+// mpcqp_common.h -- shared device primitives, layouts and the launch record of the batched
+// MPC QP solver (included by mpcqp.hip and by the per-horizon solver objects).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdint>
+#include <cstdio>
+#include <cstring>
+#include <new>
+#include <string>
+#include <type_traits>
+#include <utility>
+
+#include "../../include/mpcqp.h"
+
+namespace {
+
+constexpr int kWave = 64;
+constexpr double kPi = 3.141592653589793;
+constexpr double kTwoPi = 6.283185307179586;
+constexpr double kMinScaling = 1e-4;
+constexpr double kMaxScaling = 1e4;
+constexpr double kRhoMin = 1e-6;
+constexpr double kRhoMax = 1e6;
+constexpr double kDivTol = 1e-30;
+constexpr double kRank1Min = 1e-10;  // smallest 1 + delta c'A^{-1}c accepted by a rank-1 update
+
+// ------------------------------------------------------------------ layouts
+__host__ __device__ constexpr int model_stride(int N) { return ((11 * N + 10) + 7) / 8 * 8; }
+
+// Solver state per QP (doubles):
+//   [0, n*n)            Pbar, symmetric, row-major
+//   lane fields         kF* x 64 doubles, lane-contiguous
+//   scalars             cscale, admm_ok, admm_it, n_fact
+enum LaneField {
+  kFq = 0,
+  kFD,
+  kFx,
+  kFE0,
+  kFE1,
+  kFE2,
+  kFlo0,
+  kFlo1,
+  kFlo2,
+  kFhi0,
+  kFhi1,
+  kFhi2,
+  kFw0,
+  kFw1,
+  kFw2,
+  kNumFields
+};
+__host__ __device__ constexpr int state_lane_off(int N) { return (4 * N * N + 7) / 8 * 8; }
+__host__ __device__ constexpr int state_scal_off(int N) { return state_lane_off(N) + kNumFields * kWave; }
+__host__ __device__ constexpr int state_stride(int N) { return state_scal_off(N) + 8; }
+
+// ------------------------------------------------------------------ wave primitives (DPP)
+template <int CTRL>
+__device__ __forceinline__ double dpp(double v) {
+  const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), CTRL, 0xf, 0xf, true);
+  const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), CTRL, 0xf, 0xf, true);
+  return __hiloint2double(hi, lo);
+}
+__device__ __forceinline__ double readlane(double v, int l) {
+  return __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(v), l),
+                          __builtin_amdgcn_readlane(__double2loint(v), l));
+}
+constexpr int kRowShr1 = 0x111, kRowShr2 = 0x112, kRowShr4 = 0x114, kRowShr8 = 0x118;
+constexpr int kRowShl1 = 0x101, kRowShl2 = 0x102, kRowShl4 = 0x104, kRowShl8 = 0x108;
+constexpr int kWaveShr1 = 0x138, kWaveShl1 = 0x130;
+
+// inclusive prefix sum over lanes 0..lane (zero-filled row shifts + row totals)
+__device__ __forceinline__ double scan_add(double v, int lane) {
+  v += dpp<kRowShr1>(v);
+  v += dpp<kRowShr2>(v);
+  v += dpp<kRowShr4>(v);
+  v += dpp<kRowShr8>(v);
+  const double t0 = readlane(v, 15), t1 = readlane(v, 31), t2 = readlane(v, 47);
+  const int row = lane >> 4;
+  double off = row >= 1 ? t0 : 0.0;
+  if (row >= 2) off += t1;
+  if (row >= 3) off += t2;
+  return v + off;
+}
+// inclusive suffix sum over lanes lane..63
+__device__ __forceinline__ double rscan_add(double v, int lane) {
+  v += dpp<kRowShl1>(v);
+  v += dpp<kRowShl2>(v);
+  v += dpp<kRowShl4>(v);
+  v += dpp<kRowShl8>(v);
+  const double t1 = readlane(v, 16), t2 = readlane(v, 32), t3 = readlane(v, 48);
+  const int row = lane >> 4;
+  double off = row <= 2 ? t3 : 0.0;
+  if (row <= 1) off += t2;
+  if (row <= 0) off += t1;
+  return v + off;
+}
+// inclusive prefix / suffix max of non-negative values
+__device__ __forceinline__ double scan_max(double v, int lane) {
+  v = fmax(v, dpp<kRowShr1>(v));
+  v = fmax(v, dpp<kRowShr2>(v));
+  v = fmax(v, dpp<kRowShr4>(v));
+  v = fmax(v, dpp<kRowShr8>(v));
+  const double t0 = readlane(v, 15), t1 = readlane(v, 31), t2 = readlane(v, 47);
+  const int row = lane >> 4;
+  double off = row >= 1 ? t0 : 0.0;
+  if (row >= 2) off = fmax(off, t1);
+  if (row >= 3) off = fmax(off, t2);
+  return fmax(v, off);
+}
+__device__ __forceinline__ double rscan_max(double v, int lane) {
+  v = fmax(v, dpp<kRowShl1>(v));
+  v = fmax(v, dpp<kRowShl2>(v));
+  v = fmax(v, dpp<kRowShl4>(v));
+  v = fmax(v, dpp<kRowShl8>(v));
+  const double t1 = readlane(v, 16), t2 = readlane(v, 32), t3 = readlane(v, 48);
+  const int row = lane >> 4;
+  double off = row <= 2 ? t3 : 0.0;
+  if (row <= 1) off = fmax(off, t2);
+  if (row <= 0) off = fmax(off, t1);
+  return fmax(v, off);
+}
+// wave-uniform sum / max (row scans + four row totals)
+__device__ __forceinline__ double wave_sum(double v) {
+  v += dpp<kRowShr1>(v);
+  v += dpp<kRowShr2>(v);
+  v += dpp<kRowShr4>(v);
+  v += dpp<kRowShr8>(v);
+  return (readlane(v, 15) + readlane(v, 31)) + (readlane(v, 47) + readlane(v, 63));
+}
+__device__ __forceinline__ double wave_max(double v) {  // v >= 0
+  v = fmax(v, dpp<kRowShr1>(v));
+  v = fmax(v, dpp<kRowShr2>(v));
+  v = fmax(v, dpp<kRowShr4>(v));
+  v = fmax(v, dpp<kRowShr8>(v));
+  return fmax(fmax(readlane(v, 15), readlane(v, 31)), fmax(readlane(v, 47), readlane(v, 63)));
+}
+// lane i <- lane i-2 (0 for i < 2);  lane i <- lane i+2 (0 past the wave)
+__device__ __forceinline__ double shr2(double v) { return dpp<kWaveShr1>(dpp<kWaveShr1>(v)); }
+__device__ __forceinline__ double shl2(double v) { return dpp<kWaveShl1>(dpp<kWaveShl1>(v)); }
+__device__ __forceinline__ bool wave_any(bool b) { return __ballot(b) != 0ull; }
+
+// ---- register broadcasts for the dense row-per-lane products (no LDS)
+// A dense product over a vector v distributed one element per lane needs every lane to see
+// every v_j.  bcast() replicates each 16-lane row of v into all four rows with the gfx950
+// permlane swaps (w[c] lane l = v[16c + (l & 15)]); v_fmac_f64 with DPP row_newbcast:L then
+// reads lane L of each row's copy as its multiplicand, so a broadcast-FMA is ONE VALU
+// instruction with no memory latency.  Must run with all 64 lanes active.
+template <int NW>  // rows needed: ceil(n / 16)
+__device__ __forceinline__ void bcast(double v, double w[4]) {
+  const int lo = __double2loint(v), hi = __double2hiint(v);
+  const auto l16 = __builtin_amdgcn_permlane16_swap(lo, lo, false, false);  // rows {0,0,2,2} / {1,1,3,3}
+  const auto h16 = __builtin_amdgcn_permlane16_swap(hi, hi, false, false);
+  const auto la = __builtin_amdgcn_permlane32_swap(l16[0], l16[0], false, false);  // row 0 x4 / row 2 x4
+  const auto ha = __builtin_amdgcn_permlane32_swap(h16[0], h16[0], false, false);
+  w[0] = __hiloint2double(ha[0], la[0]);
+  if constexpr (NW > 1) {
+    const auto lb = __builtin_amdgcn_permlane32_swap(l16[1], l16[1], false, false);  // row 1 x4 / row 3 x4
+    const auto hb = __builtin_amdgcn_permlane32_swap(h16[1], h16[1], false, false);
+    w[1] = __hiloint2double(hb[0], lb[0]);
+    if constexpr (NW > 3) w[3] = __hiloint2double(hb[1], lb[1]);
+  }
+  if constexpr (NW > 2) w[2] = __hiloint2double(ha[1], la[1]);
+  // DPP reads of a VGPR need two wait states after its VALU write; tie the pad to w
+  if constexpr (NW == 1) asm volatile("s_nop 1" : "+v"(w[0]));
+  if constexpr (NW == 2) asm volatile("s_nop 1" : "+v"(w[0]), "+v"(w[1]));
+  if constexpr (NW == 3) asm volatile("s_nop 1" : "+v"(w[0]), "+v"(w[1]), "+v"(w[2]));
+  if constexpr (NW == 4) asm volatile("s_nop 1" : "+v"(w[0]), "+v"(w[1]), "+v"(w[2]), "+v"(w[3]));
+}
+// acc += w[lane 16*row + L] * m   (one v_fmac_f64_dpp)
+template <int L>
+__device__ __forceinline__ void fmac_bc(double& acc, double w, double m) {
+  asm("v_fmac_f64_dpp %0, %1, %2 row_newbcast:%3 row_mask:0xf bank_mask:0xf" : "+v"(acc) : "v"(w), "v"(m), "i"(L));
+}
+// compile-time loop: f(std::integral_constant<int, I>) for I in [B, E)
+template <int B, int E>
+struct Unroll {
+  template <class F>
+  __device__ __forceinline__ static void run(F&& f) {
+    if constexpr (B < E) {
+      f(std::integral_constant<int, B>{});
+      Unroll<B + 1, E>::run(f);
+    }
+  }
+};
+
+// Every kernel runs one wavefront per workgroup, and the LDS operations of one wavefront
+// execute in program order: a broadcast through LDS needs only a compiler-level ordering
+// point (wavefront-scope fence), not an s_barrier with its lgkmcnt(0) drain.
+__device__ __forceinline__ void lds_sync() { __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront"); }
+
+// ------------------------------------------------------------------ diagnostic stamps
+// Built only with -DMPCQP_STAMPS (never in the measured library): per-phase s_memtime
+// cycle sums, flushed once per wave into g_stamps[] (read by mpcqp_debug_stamps).
+#ifdef MPCQP_STAMPS
+__device__ unsigned long long g_stamps[16];
+struct Stamps {
+  unsigned long long acc[6] = {0, 0, 0, 0, 0, 0};
+  unsigned long long t = 0;
+  __device__ __forceinline__ void begin() {
+    __builtin_amdgcn_sched_barrier(0);
+    t = __builtin_amdgcn_s_memtime();
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  __device__ __forceinline__ void end(int s) {
+    __builtin_amdgcn_sched_barrier(0);
+    acc[s] += __builtin_amdgcn_s_memtime() - t;
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  __device__ __forceinline__ void flush(int base) {
+    if (threadIdx.x == 0)
+      for (int s = 0; s < 6; ++s) atomicAdd(&g_stamps[base + s], acc[s]);
+  }
+};
+#else
+struct Stamps {
+  __device__ __forceinline__ void begin() {}
+  __device__ __forceinline__ void end(int) {}
+  __device__ __forceinline__ void flush(int) {}
+};
+#endif
+
+__device__ __forceinline__ double limit_scaling(double v) {
+  return v < kMinScaling ? 1.0 : (v > kMaxScaling ? kMaxScaling : v);
+}
+
+// numpy float mod (npy_divmod) for b > 0
+__device__ __forceinline__ double np_mod(double a, double b) {
+  double m = fmod(a, b);
+  if (m != 0.0) {
+    if (m < 0.0) m += b;
+  } else {
+    m = 0.0;
+  }
+  return m;
+}
+
+}  // namespace
+
+namespace mpcqp {
+// One solve launch (device pointers; outputs may be null).
+struct Launch {
+  const mpcqp_params* p;
+  int B;
+  const double* model;
+  double* state;
+  double *u0, *X, *U;
+  int32_t *st, *it;
+  uint8_t* ac;
+};
+
+typedef void (*launcher_t)(hipStream_t, const Launch&);
+// K2a -> K2b -> K2c for horizon N; defined in mpcqp_solve.h, instantiated per horizon in
+// mpcqp_part.hip objects (parallel build) or in mpcqp.hip itself (MPCQP_ONLY_N dev builds).
+template <int N>
+void launch_solve(hipStream_t s, const Launch& L);
+}  // namespace mpcqp

@@ -1,0 +1,861 @@
+// mpcqp_solve.h -- K2a/K2b/K2c solver kernels, templated on the horizon N.
+#pragma once
+#include "mpcqp_common.h"
+
+namespace {
+using mpcqp::Launch;
+
+template <int N>
+struct SetupSmem {
+  static constexpr int n = 2 * N;
+  static constexpr int LD = n + 1;  // odd: conflict-free row and column access
+  double P[n * LD];
+  double buf[kWave];
+  double model[model_stride(N)];
+  double pre[4][N + 1];  // prefix sums of alpha, beta, gamma, eta
+  double err[N + 1][4];  // free-response tracking error e_m = sx_m - r_m
+  double g[n];
+};
+
+template <int N>
+__global__ __launch_bounds__(kWave) void k_setup(mpcqp_params p, int B, const double* __restrict__ model,
+                                                 double* __restrict__ state) {
+  constexpr int n = 2 * N;
+  constexpr int LD = SetupSmem<N>::LD;
+  constexpr int S = model_stride(N);
+  __shared__ SetupSmem<N> sm;
+  const int b = blockIdx.x;
+  const int lane = threadIdx.x;
+  if (b >= B) return;
+  const bool act = lane < n;
+  const bool even = act && ((lane & 1) == 0);
+  const int cc = lane & 1;  // 0 = acceleration, 1 = steering
+  const double dt = p.dt;
+
+  {
+    const double* mb = model + (size_t)b * S;
+    for (int i = lane; i < S; i += kWave) sm.model[i] = mb[i];
+  }
+  __syncthreads();
+  const double* al = sm.model;
+  const double* be = sm.model + N;
+  const double* ga = sm.model + 2 * N;
+  const double* et = sm.model + 3 * N;
+  const double* si = sm.model + 4 * N;
+  const double* c0 = sm.model + 5 * N;
+  const double* c1 = sm.model + 6 * N;
+  const double* rr = sm.model + 7 * N;
+  const double* x0 = sm.model + 11 * N + 4;
+  const double* up = sm.model + 11 * N + 8;
+
+  // prefix sums (lanes 0..3, one array each) and free response (lane 4)
+  if (lane < 4) {
+    const double* a = sm.model + lane * N;
+    double acc = 0.0;
+    sm.pre[lane][0] = 0.0;
+    for (int k = 0; k < N; ++k) {
+      acc += a[k];
+      sm.pre[lane][k + 1] = acc;
+    }
+  } else if (lane == 4) {
+    double px = x0[0], py = x0[1];
+    const double psi = x0[2], v = x0[3];
+    for (int m = 1; m <= N; ++m) {
+      const int k = m - 1;
+      px = px + al[k] * psi + be[k] * v + c0[k];
+      py = py + ga[k] * psi + et[k] * v + c1[k];
+      sm.err[m][0] = px - rr[4 * m + 0];
+      sm.err[m][1] = py - rr[4 * m + 1];
+      sm.err[m][2] = psi - rr[4 * m + 2];
+      sm.err[m][3] = v - rr[4 * m + 3];
+    }
+  }
+  __syncthreads();
+
+  // ---- condense: column `lane` of H (lane n -> g) by the backward adjoint recursion ----
+  // mu_m = W_m s_m + A_m' mu_{m+1};  H[(i,c'), col] = (B_i e_c')' mu_{i+1}
+  if (lane <= n) {
+    double Q[4][4], QN[4][4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        Q[i][j] = 0.5 * (p.q[4 * i + j] + p.q[4 * j + i]);
+        QN[i][j] = 0.5 * (p.q_terminal[4 * i + j] + p.q_terminal[4 * j + i]);
+      }
+    const int j = lane >> 1;
+    const bool gcol = lane == n;
+    const double sj = gcol ? 0.0 : si[j];
+    const double pa0 = gcol ? 0.0 : sm.pre[0][j + 1], pb0 = gcol ? 0.0 : sm.pre[1][j + 1];
+    const double pg0 = gcol ? 0.0 : sm.pre[2][j + 1], pe0 = gcol ? 0.0 : sm.pre[3][j + 1];
+    double mu0 = 0.0, mu1 = 0.0, mu2 = 0.0, mu3 = 0.0;
+    for (int m = N; m >= 1; --m) {
+      double s0, s1, s2, s3;
+      if (gcol) {
+        s0 = sm.err[m][0];
+        s1 = sm.err[m][1];
+        s2 = sm.err[m][2];
+        s3 = sm.err[m][3];
+      } else if (m > j) {
+        if (cc == 0) {
+          s0 = dt * (sm.pre[1][m] - pb0);
+          s1 = dt * (sm.pre[3][m] - pe0);
+          s2 = 0.0;
+          s3 = dt;
+        } else {
+          s0 = sj * (sm.pre[0][m] - pa0);
+          s1 = sj * (sm.pre[2][m] - pg0);
+          s2 = sj;
+          s3 = 0.0;
+        }
+      } else {
+        s0 = s1 = s2 = s3 = 0.0;
+      }
+      const bool term = m == N;
+      auto W = [&](int i, int k) -> double { return term ? QN[i][k] : Q[i][k]; };
+      const double w0 = W(0, 0) * s0 + W(0, 1) * s1 + W(0, 2) * s2 + W(0, 3) * s3;
+      const double w1 = W(1, 0) * s0 + W(1, 1) * s1 + W(1, 2) * s2 + W(1, 3) * s3;
+      const double w2 = W(2, 0) * s0 + W(2, 1) * s1 + W(2, 2) * s2 + W(2, 3) * s3;
+      const double w3 = W(3, 0) * s0 + W(3, 1) * s1 + W(3, 2) * s2 + W(3, 3) * s3;
+      if (m < N) {
+        const double m0 = mu0, m1 = mu1;
+        mu0 = w0 + m0;
+        mu1 = w1 + m1;
+        mu2 = w2 + (mu2 + al[m] * m0 + ga[m] * m1);
+        mu3 = w3 + (mu3 + be[m] * m0 + et[m] * m1);
+      } else {
+        mu0 = w0;
+        mu1 = w1;
+        mu2 = w2;
+        mu3 = w3;
+      }
+      const double ha = dt * mu3, hd = si[m - 1] * mu2;
+      if (gcol) {
+        sm.g[2 * (m - 1)] = ha;
+        sm.g[2 * (m - 1) + 1] = hd;
+      } else {
+        sm.P[(2 * (m - 1)) * LD + lane] = ha;
+        sm.P[(2 * (m - 1) + 1) * LD + lane] = hd;
+      }
+    }
+    if (!gcol) {
+      const double R0 = 0.5 * (p.r[0 * 2 + cc] + p.r[cc * 2 + 0]);
+      const double R1 = 0.5 * (p.r[1 * 2 + cc] + p.r[cc * 2 + 1]);
+      sm.P[(2 * j) * LD + lane] += R0;
+      sm.P[(2 * j + 1) * LD + lane] += R1;
+    }
+  }
+  __syncthreads();
+
+  // ---- unscaled data: P = 2H (column `lane`), q = 2g, folded row bounds ----
+  double qv = act ? 2.0 * sm.g[lane] : 0.0;
+  double cmax = 0.0;  // running column max of |P|
+  if (act) {
+#pragma unroll 8
+    for (int i = 0; i < n; ++i) {
+      const double t = 2.0 * sm.P[i * LD + lane];
+      sm.P[i * LD + lane] = t;
+      cmax = fmax(cmax, fabs(t));
+    }
+  }
+  double lo[3], hi[3], wt[3], E[3];
+  {
+    const double off = lane < 2 ? up[cc] : 0.0;
+    lo[0] = even ? p.v_bounds[0] - x0[3] : 0.0;
+    hi[0] = even ? p.v_bounds[1] - x0[3] : 0.0;
+    wt[0] = even ? p.slack_velocity : 0.0;
+    lo[1] = act ? p.u_bounds[2 * cc] : 0.0;
+    hi[1] = act ? p.u_bounds[2 * cc + 1] : 0.0;
+    wt[1] = act ? p.slack_input : 0.0;
+    lo[2] = act ? p.du_bounds[2 * cc] + off : 0.0;
+    hi[2] = act ? p.du_bounds[2 * cc + 1] + off : 0.0;
+    wt[2] = act ? p.slack_rate : 0.0;
+    E[0] = even ? 1.0 : 0.0;
+    E[1] = act ? 1.0 : 0.0;
+    E[2] = act ? 1.0 : 0.0;
+  }
+  double D = act ? 1.0 : 0.0;
+  double cscale = 1.0;
+
+  // ---- Ruiz equilibration + cost scaling (OSQP scale_data, `scaling` iterations) ----
+  for (int it = 0; it < p.scaling; ++it) {
+    // column norms of [P; A] (first n columns of the KKT matrix)
+    const double sufE = rscan_max(E[0], lane);  // max E over v rows >= p/2 (odd lanes carry 0)
+    const double e2n = shl2(E[2]);
+    double ccol = fmax(E[1], E[2]);
+    if (lane + 2 < n) ccol = fmax(ccol, e2n);
+    if (even) ccol = fmax(ccol, dt * sufE);
+    ccol *= D;
+    const double dl = act ? 1.0 / sqrt(limit_scaling(fmax(cmax, ccol))) : 0.0;
+    // row norms of A
+    const double preD = scan_max(even ? D : 0.0, lane);
+    const double Dm2 = shr2(D);
+    const double el0 = even ? 1.0 / sqrt(limit_scaling(E[0] * dt * preD)) : 0.0;
+    const double el1 = act ? 1.0 / sqrt(limit_scaling(E[1] * D)) : 0.0;
+    const double el2 = act ? 1.0 / sqrt(limit_scaling(E[2] * (lane >= 2 ? fmax(D, Dm2) : D))) : 0.0;
+    // apply: P <- dl P dl (column `lane`), q <- dl q
+    __syncthreads();
+    sm.buf[lane] = dl;
+    __syncthreads();
+    double cm2 = 0.0;
+    if (act) {
+#pragma unroll 8
+      for (int i = 0; i < n; ++i) {
+        const double t = sm.P[i * LD + lane] * (sm.buf[i] * dl);
+        sm.P[i * LD + lane] = t;
+        cm2 = fmax(cm2, fabs(t));
+      }
+    }
+    D *= dl;
+    qv *= dl;
+    E[0] *= el0;
+    E[1] *= el1;
+    E[2] *= el2;
+    // cost scaling
+    const double cn = wave_sum(act ? cm2 : 0.0) / n;
+    const double qn = limit_scaling(wave_max(fabs(qv)));
+    const double ct = 1.0 / limit_scaling(fmax(cn, qn));
+    if (act) {
+#pragma unroll 8
+      for (int i = 0; i < n; ++i) sm.P[i * LD + lane] *= ct;
+    }
+    qv *= ct;
+    cmax = cm2 * ct;
+    cscale *= ct;
+  }
+  __syncthreads();
+
+  // ---- write the solver state ----
+  double* st = state + (size_t)b * state_stride(N);
+  bool finite = isfinite(qv) && isfinite(cscale);
+  if (act) {
+    // symmetric Pbar: the lower-triangle value (computed by column `min`) for both halves
+    for (int i = 0; i < n; ++i) {
+      const double v = i >= lane ? sm.P[i * LD + lane] : sm.P[lane * LD + i];
+      finite = finite && isfinite(v);
+      st[i * n + lane] = v;
+    }
+  }
+  double* lf = st + state_lane_off(N);
+  double wb[3];
+#pragma unroll
+  for (int r = 0; r < 3; ++r) {
+    lo[r] *= E[r];
+    hi[r] *= E[r];
+    wb[r] = E[r] > 0.0 ? cscale * wt[r] / (E[r] * E[r]) : 0.0;
+    finite = finite && isfinite(lo[r]) && isfinite(hi[r]);
+  }
+  // non-finite data (NaN/inf in x0, ref or u_prev) -> status MPCQP_NUMERICAL_ERROR
+  const bool bad_input = wave_any(!finite);
+  lf[kFq * kWave + lane] = qv;
+  lf[kFD * kWave + lane] = D;
+  lf[kFx * kWave + lane] = 0.0;
+#pragma unroll
+  for (int r = 0; r < 3; ++r) {
+    lf[(kFE0 + r) * kWave + lane] = E[r];
+    lf[(kFlo0 + r) * kWave + lane] = lo[r];
+    lf[(kFhi0 + r) * kWave + lane] = hi[r];
+    lf[(kFw0 + r) * kWave + lane] = wb[r];
+  }
+  if (lane == 0) {
+    double* sc = st + state_scal_off(N);
+    sc[0] = cscale;
+    sc[1] = bad_input ? -1.0 : 0.0;  // ADMM flag: -1 numerical error, 0 not converged, 1 converged
+    sc[2] = 0.0;                     // admm iterations
+    sc[3] = 0.0;                     // factorizations
+  }
+}
+
+// ------------------------------------------------------------------ shared solver context
+// Per-lane view of one scaled QP plus the structured operators and the KKT inverse.
+template <int N>
+struct Ctx {
+  static constexpr int n = 2 * N;
+  int lane;
+  bool act, even;
+  double dt;
+  double D, qv;
+  double E[3], lo[3], hi[3], wb[3];
+  double cscale;
+  const double* __restrict__ P;  // Pbar (global, L2-resident)
+  double* buf;                   // LDS broadcast buffer, >= 2*kWave doubles
+  double* sv;                    // LDS, N+1 doubles
+  double* Dl;                    // LDS copy of D (n doubles)
+  static constexpr int kNW = (n + 15) / 16;  // 16-lane rows holding the n variables
+  // KKT inverse, row `lane`: A^{-1}[lane][j] = -r[j] (symmetric sweep operator)
+  double r[n];
+
+  __device__ __forceinline__ void load(const double* st, int ln, double dt_, double* buf_, double* sv_, double* Dl_,
+                                       double* Ps) {
+    lane = ln;
+    act = ln < n;
+    even = act && ((ln & 1) == 0);
+    dt = dt_;
+    buf = buf_;
+    sv = sv_;
+    Dl = Dl_;
+    // Pbar is re-read by every factorization and every P-product: stage it in LDS once
+    for (int i = ln; i < n * n; i += kWave) Ps[i] = st[i];
+    P = Ps;
+    const double* lf = st + state_lane_off(N);
+    qv = lf[kFq * kWave + ln];
+    D = lf[kFD * kWave + ln];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      E[k] = lf[(kFE0 + k) * kWave + ln];
+      lo[k] = lf[(kFlo0 + k) * kWave + ln];
+      hi[k] = lf[(kFhi0 + k) * kWave + ln];
+      wb[k] = lf[(kFw0 + k) * kWave + ln];
+    }
+    cscale = st[state_scal_off(N)];
+    if (act) Dl[ln] = D;
+    __syncthreads();
+  }
+
+  // Make the per-lane problem data opaque to the optimizer at the top of a solver
+  // iteration: otherwise LICM hoists dozens of derived values (reciprocals, products,
+  // masks) out of the loops and the kernel drops to one wave per SIMD.
+  __device__ __forceinline__ void opaque() {
+    asm volatile("" : "+v"(D), "+v"(qv), "+v"(lane));
+    asm volatile("" : "+v"(E[0]), "+v"(E[1]), "+v"(E[2]));
+    asm volatile("" : "+v"(lo[0]), "+v"(lo[1]), "+v"(lo[2]));
+    asm volatile("" : "+v"(hi[0]), "+v"(hi[1]), "+v"(hi[2]));
+    asm volatile("" : "+v"(wb[0]), "+v"(wb[1]), "+v"(wb[2]));
+  }
+
+  // z = Cbar x
+  __device__ __forceinline__ void Cmul(double x, double z[3]) const {
+    const double t = D * x;
+    const double pre = scan_add(even ? t : 0.0, lane);
+    const double tm2 = shr2(t);
+    z[0] = E[0] * dt * pre;
+    z[1] = E[1] * t;
+    z[2] = E[2] * (lane >= 2 ? t - tm2 : t);
+  }
+  // x = Cbar' y
+  __device__ __forceinline__ double CTmul(const double y[3]) const {
+    const double suf = rscan_add(E[0] * y[0], lane);
+    const double ey2 = E[2] * y[2];
+    const double n2 = shl2(ey2);
+    double t = (even ? dt * suf : 0.0) + E[1] * y[1] + ey2;
+    if (lane + 2 < n) t -= n2;
+    return act ? D * t : 0.0;
+  }
+  // (Pbar v)_lane, Pbar symmetric: lane reads its row as a conflict-free column of the LDS copy
+  __device__ __forceinline__ double Pmul(double v) const {
+    double w[4];
+    bcast<kNW>(act ? v : 0.0, w);
+    const int col = act ? lane : 0;
+    double a[4] = {0.0, 0.0, 0.0, 0.0};
+    Unroll<0, n>::run([&](auto jc) {
+      constexpr int j = decltype(jc)::value;
+      fmac_bc<j % 16>(a[j % 4], w[j / 16], P[j * n + col]);
+    });
+    return act ? (a[0] + a[1]) + (a[2] + a[3]) : 0.0;
+  }
+  // KKT matrix A = Pbar + s I + Cbar' diag(rw) Cbar, row `lane` -> r[]
+  __device__ __forceinline__ void form(double s, const double rw[3]) {
+    // opaque lane copy: keeps per-column masks/addresses from being hoisted out of solver loops
+    int ln = lane;
+    asm volatile("" : "+v"(ln));
+    const bool ev_ln = ln < n && (ln & 1) == 0;
+    const double ev = E[0] * E[0] * rw[0];
+    const double suf = rscan_add(even ? ev : 0.0, lane);  // sum over v rows >= lane/2
+    const double du2 = E[2] * E[2] * rw[2];
+    const double du2n = shl2(du2);
+    lds_sync();
+    if (even) sv[lane >> 1] = suf;
+    lds_sync();
+    double diag = E[1] * E[1] * rw[1] + du2;
+    if (ln + 2 < n) diag += du2n;
+    const int col = ln < n ? ln : 0;
+    const double Dm = ln < n ? D : 0.0;
+    double wD[4];
+    bcast<kNW>(Dm, wD);  // D_j of every lane j
+    Unroll<0, n>::run([&](auto jc) {
+      constexpr int j = decltype(jc)::value;
+      double t = 0.0;
+      if ((j & 1) == 0 && ev_ln) {
+        const int mx = (ln > j ? ln : j) >> 1;
+        t = dt * dt * sv[mx];
+      }
+      if (j == ln) t += diag;
+      if (j == ln + 2) t -= du2n;
+      if (j + 2 == ln) t -= du2;
+      double v = ln < n ? P[j * n + col] + (j == ln ? s : 0.0) : 0.0;
+      fmac_bc<j % 16>(v, wD[j / 16], Dm * t);
+      r[j] = v;
+    });
+  }
+  // Symmetric sweep operator on the rows in r[]: afterwards A^{-1} = -r (row `lane`).
+  // Step k: every lane needs its own A[i][k] (register r[k]) and the pivot row A[k][j] =
+  // A[j][k] (symmetry) -- the column r[k] of all lanes, register-broadcast by bcast() and read
+  // through DPP row_newbcast, so each update r[j] += coef * A[k][j] is one v_fmac_f64_dpp.
+  // The pivot row itself is the same FMA with coef = 1/d - 1 (A[k][j] <- A[k][j] / d), so the
+  // update is uniform over lanes.  The step loop is unrolled at compile time (static register
+  // indices and DPP lane immediates).  false on a non-positive pivot.
+  __device__ __forceinline__ bool sweep() {
+    bool ok = true;
+    Unroll<0, n>::run([&](auto kc) {
+      constexpr int k = decltype(kc)::value;
+      double w[4];
+      bcast<kNW>(r[k], w);
+      const double d = readlane(r[k], k);
+      ok = ok && (d > 0.0) && isfinite(d);
+      const double inv = 1.0 / d;
+      const bool piv = lane == k;
+      const double ck = r[k] * inv;
+      const double coef = piv ? inv - 1.0 : -ck;
+      // next pivot column first: the next step's broadcast depends only on it
+      if constexpr (k + 1 < n) fmac_bc<(k + 1) % 16>(r[k + 1], w[(k + 1) / 16], coef);
+      Unroll<0, n>::run([&](auto jc) {
+        constexpr int j = decltype(jc)::value;
+        if constexpr (j != k && j != k + 1) fmac_bc<j % 16>(r[j], w[j / 16], coef);
+      });
+      r[k] = piv ? -inv : ck;
+    });
+    return ok;
+  }
+  // Rank-1 change of the factorized matrix, A' = A + delta c c' with c the row (tau, l) of
+  // Cbar (Sherman-Morrison): A'^{-1} = A^{-1} - kappa u u', u = A^{-1} c,
+  // kappa = delta / (1 + delta c'u).  Used by the polish when a few soft rows enter or leave
+  // the active set.  false (inverse untouched) when 1 + delta c'u is not safely positive.
+  __device__ __forceinline__ bool rank1(int tau, int l, double delta) {
+    const double e = readlane(tau == 0 ? E[0] : (tau == 1 ? E[1] : E[2]), l);
+    double c = 0.0;
+    if (tau == 0)
+      c = (even && lane <= l) ? e * dt * D : 0.0;
+    else if (tau == 1)
+      c = lane == l ? e * D : 0.0;
+    else
+      c = lane == l ? e * D : (lane + 2 == l ? -e * D : 0.0);
+    if (!act) c = 0.0;
+    const double u = inv_mul(c);
+    const double den = 1.0 + delta * wave_sum(c * u);
+    if (!(den > kRank1Min) || !isfinite(den)) return false;
+    const double m = (delta / den) * u;
+    double w[4];
+    bcast<kNW>(u, w);
+    Unroll<0, n>::run([&](auto jc) {
+      constexpr int j = decltype(jc)::value;
+      fmac_bc<j % 16>(r[j], w[j / 16], m);
+    });
+    return true;
+  }
+  // (A^{-1} v)_lane
+  __device__ __forceinline__ double inv_mul(double v) const {
+    double w[4];
+    bcast<kNW>(act ? v : 0.0, w);
+    double a[4] = {0.0, 0.0, 0.0, 0.0};
+    Unroll<0, n>::run([&](auto jc) {
+      constexpr int j = decltype(jc)::value;
+      fmac_bc<j % 16>(a[j % 4], w[j / 16], r[j]);
+    });
+    return act ? -((a[0] + a[1]) + (a[2] + a[3])) : 0.0;
+  }
+};
+
+template <int N>
+struct SolveSmem {
+  double P[4 * N * N];  // Pbar, row-major n x n (column reads by lane are conflict-free)
+  double buf[2 * kWave];
+  double sv[N + 1];
+  double Dl[2 * N];
+};
+
+// ------------------------------------------------------------------ K2b: ADMM
+template <int N>
+__global__ __launch_bounds__(kWave) void k_admm(mpcqp_params p, int B, double* __restrict__ state) {
+  __shared__ SolveSmem<N> sm;
+  const int b = blockIdx.x;
+  if (b >= B) return;
+  double* st = state + (size_t)b * state_stride(N);
+  Ctx<N> C;
+  C.load(st, threadIdx.x, p.dt, sm.buf, sm.sv, sm.Dl, sm.P);
+  const bool act = C.act;
+  double x = 0.0, z[3] = {0.0, 0.0, 0.0}, y[3] = {0.0, 0.0, 0.0};
+  double rho = p.rho;
+  const double sg = p.sigma, alpha = p.alpha;
+  bool bad = st[state_scal_off(N) + 1] < 0.0;  // non-finite problem data (k_setup)
+  bool ok = false;
+  int it = 0, nfact = 0;
+  Stamps T, T2;
+  T2.begin();
+  while (it < p.max_iter && !bad && !ok) {
+    {
+      const double rw[3] = {rho, rho, rho};
+      T.begin();
+      C.form(sg, rw);
+      T.end(0);
+      ++nfact;
+      T.begin();
+      const bool okf = C.sweep();
+      T.end(1);
+      if (wave_any(!okf)) {
+        bad = true;
+        break;
+      }
+    }
+    bool refactor = false;
+    double prox_a[3], prox_b[3];  // zn = (rho vv + 2 w bnd) / (rho + 2 w)
+#pragma unroll
+    for (int r = 0; r < 3; ++r) {
+      prox_a[r] = rho / (rho + 2.0 * C.wb[r]);
+      prox_b[r] = 2.0 * C.wb[r] / (rho + 2.0 * C.wb[r]);
+    }
+    const double ir = 1.0 / rho;
+    while (!refactor && it < p.max_iter) {
+      ++it;
+      C.opaque();
+      T.begin();
+      double tmp[3];
+#pragma unroll
+      for (int r = 0; r < 3; ++r) tmp[r] = rho * z[r] - y[r];
+      const double rhs = C.CTmul(tmp) + sg * x - C.qv;
+      const double xt = C.inv_mul(rhs);
+      double zt[3];
+      C.Cmul(xt, zt);
+      x = alpha * xt + (1.0 - alpha) * x;
+#pragma unroll
+      for (int r = 0; r < 3; ++r) {
+        const double v = alpha * zt[r] + (1.0 - alpha) * z[r];
+        const double vv = v + y[r] * ir;
+        double zn = vv;
+        if (vv > C.hi[r])
+          zn = prox_a[r] * vv + prox_b[r] * C.hi[r];
+        else if (vv < C.lo[r])
+          zn = prox_a[r] * vv + prox_b[r] * C.lo[r];
+        y[r] = y[r] + rho * (v - zn);
+        z[r] = zn;
+      }
+      T.end(2);
+      if (it % p.check_termination == 0 || it == p.max_iter) {
+        T.begin();
+        double Ax[3];
+        C.Cmul(x, Ax);
+        const double Px = C.Pmul(x);
+        const double Aty = C.CTmul(y);
+        double pr = 0, nAx = 0, nz = 0, spr = 0, snAx = 0, snz = 0;
+#pragma unroll
+        for (int r = 0; r < 3; ++r) {
+          if (C.E[r] > 0.0) {
+            const double ie = 1.0 / C.E[r];
+            pr = fmax(pr, fabs((Ax[r] - z[r]) * ie));
+            nAx = fmax(nAx, fabs(Ax[r] * ie));
+            nz = fmax(nz, fabs(z[r] * ie));
+            spr = fmax(spr, fabs(Ax[r] - z[r]));
+            snAx = fmax(snAx, fabs(Ax[r]));
+            snz = fmax(snz, fabs(z[r]));
+          }
+        }
+        double du = 0, nPx = 0, nAty = 0, nq = 0, sdu = 0, snPx = 0, snAty = 0, snq = 0;
+        if (act) {
+          const double id = 1.0 / C.D;
+          const double rd = Px + C.qv + Aty;
+          du = fabs(rd * id);
+          nPx = fabs(Px * id);
+          nAty = fabs(Aty * id);
+          nq = fabs(C.qv * id);
+          sdu = fabs(rd);
+          snPx = fabs(Px);
+          snAty = fabs(Aty);
+          snq = fabs(C.qv);
+        }
+        pr = wave_max(pr);
+        nAx = wave_max(nAx);
+        nz = wave_max(nz);
+        du = wave_max(du);
+        nPx = wave_max(nPx);
+        nAty = wave_max(nAty);
+        nq = wave_max(nq);
+        const double ic = 1.0 / C.cscale;
+        du *= ic;
+        const double ep = p.eps_abs + p.eps_rel * fmax(nAx, nz);
+        const double ed = p.eps_abs + p.eps_rel * fmax(fmax(nPx, nAty), nq) * ic;
+        T.end(3);
+        // fmax drops NaNs, so test the iterate itself
+        if (wave_any(!isfinite(x) || !isfinite(z[0] + z[1] + z[2]) || !isfinite(y[0] + y[1] + y[2])) ||
+            !isfinite(pr) || !isfinite(du)) {
+          bad = true;
+          break;
+        }
+        if (pr <= ep && du <= ed) {
+          ok = true;
+          break;
+        }
+        if (p.adaptive_rho && it % p.adaptive_rho_interval == 0) {
+          spr = wave_max(spr);
+          snAx = wave_max(snAx);
+          snz = wave_max(snz);
+          sdu = wave_max(sdu);
+          snPx = wave_max(snPx);
+          snAty = wave_max(snAty);
+          snq = wave_max(snq);
+          const double pn = spr / (fmax(snAx, snz) + kDivTol);
+          const double dn = sdu / (fmax(fmax(snPx, snAty), snq) + kDivTol);
+          double rn = rho * sqrt(pn / (dn + kDivTol));
+          rn = fmin(fmax(rn, kRhoMin), kRhoMax);
+          if (rn > rho * p.adaptive_rho_tolerance || rn < rho / p.adaptive_rho_tolerance) {
+            rho = rn;
+            refactor = true;
+          }
+        }
+      }
+    }
+  }
+  double* lf = st + state_lane_off(N);
+  lf[kFx * kWave + threadIdx.x] = act ? x : 0.0;
+  if (threadIdx.x == 0) {
+    double* sc = st + state_scal_off(N);
+    sc[1] = bad ? -1.0 : (ok ? 1.0 : 0.0);
+    sc[2] = (double)it;
+    sc[3] = (double)nfact;
+  }
+  T2.end(0);
+  T.flush(0);   // g_stamps[0..3]: form, sweep, ADMM iteration body, termination checks
+  T2.flush(4);  // g_stamps[4]: whole k_admm
+}
+
+// ------------------------------------------------------------------ K2c: polish + outputs
+template <int N>
+__global__ __launch_bounds__(kWave) void k_finish(mpcqp_params p, int B, const double* __restrict__ model,
+                                                  const double* __restrict__ state, double* __restrict__ u0o,
+                                                  double* __restrict__ Xo, double* __restrict__ Uo,
+                                                  int32_t* __restrict__ statuso, int32_t* __restrict__ iterso,
+                                                  uint8_t* __restrict__ activeo) {
+  constexpr int n = 2 * N;
+  __shared__ SolveSmem<N> sm;
+  const int b = blockIdx.x;
+  if (b >= B) return;
+  const int lane = threadIdx.x;
+  const double* st = state + (size_t)b * state_stride(N);
+  Ctx<N> C;
+  C.load(st, lane, p.dt, sm.buf, sm.sv, sm.Dl, sm.P);
+  const bool act = C.act;
+  const bool use_admm = p.method == MPCQP_METHOD_ADMM;
+  const bool do_polish = !use_admm || p.polish != 0;
+  const double* sc = st + state_scal_off(N);
+  const double admm_flag = sc[1];  // -1: non-finite data (k_setup) or ADMM numerical error
+  bool bad = admm_flag < 0.0;
+  const bool admm_ok = admm_flag > 0.0;
+  const int admm_it = use_admm ? (int)sc[2] : 0;
+  int nfact = use_admm ? (int)sc[3] : 0;
+  double x = use_admm ? st[state_lane_off(N) + kFx * kWave + lane] : 0.0;
+  const double x_admm = x;
+  bool pol_ok = false;
+  int pol_it = 0, n_ls = 0;
+  Stamps T, T2;
+  T2.begin();
+
+  if (do_polish && !bad) {
+    double zc[3];
+    int cd[3];
+    C.Cmul(x, zc);
+#pragma unroll
+    for (int r = 0; r < 3; ++r) cd[r] = zc[r] > C.hi[r] ? 2 : (zc[r] < C.lo[r] ? 1 : 0);
+    constexpr int kMaxRank1 = n / 2;  // more changed rows than this: refactor (form + sweep)
+    double rwf[3] = {0.0, 0.0, 0.0};  // soft-row weights of the current factorization
+    bool have_fact = false;
+    while (pol_it < p.polish_max_iter) {
+      ++pol_it;
+      C.opaque();
+      double rw[3], tmp[3];
+#pragma unroll
+      for (int r = 0; r < 3; ++r) {
+        rw[r] = cd[r] ? 2.0 * C.wb[r] : 0.0;
+        tmp[r] = cd[r] == 2 ? rw[r] * C.hi[r] : (cd[r] == 1 ? rw[r] * C.lo[r] : 0.0);
+      }
+      // Factorize the Newton matrix of this active set: from scratch on the first pass, by
+      // rank-1 updates of the previous inverse when only a few soft rows changed.
+      bool refac = !have_fact;
+      if (!refac) {
+        uint64_t chg[3];
+        int nchg = 0;
+#pragma unroll
+        for (int r = 0; r < 3; ++r) {
+          chg[r] = __ballot(act && rw[r] != rwf[r]);
+          nchg += __popcll(chg[r]);
+        }
+        refac = nchg > kMaxRank1;
+        T.begin();
+#pragma unroll
+        for (int r = 0; r < 3; ++r) {
+          uint64_t m = chg[r];
+          while (m && !refac) {
+            const int l = __builtin_ctzll(m);
+            m &= m - 1;
+            refac = !C.rank1(r, l, readlane(rw[r] - rwf[r], l));
+          }
+        }
+        T.end(1);
+      }
+      if (refac) {
+        T.begin();
+        C.form(0.0, rw);
+        T.end(0);
+        T.begin();
+        const bool okf = C.sweep();
+        T.end(1);
+        if (wave_any(!okf)) {
+          bad = true;
+          break;
+        }
+        have_fact = true;
+      }
+      ++nfact;
+#pragma unroll
+      for (int r = 0; r < 3; ++r) rwf[r] = rw[r];
+      T.begin();
+      const double rhs = C.CTmul(tmp) - C.qv;
+      double xn = C.inv_mul(rhs);
+      {  // one step of iterative refinement: res = rhs - M xn
+        double zz[3], t3[3];
+        C.Cmul(xn, zz);
+#pragma unroll
+        for (int r = 0; r < 3; ++r) t3[r] = rw[r] * zz[r];
+        const double Mx = C.Pmul(xn) + C.CTmul(t3);
+        xn += C.inv_mul(rhs - Mx);
+      }
+      double zn[3];
+      C.Cmul(xn, zn);
+      bool diff = false;
+#pragma unroll
+      for (int r = 0; r < 3; ++r) {
+        const int c2 = zn[r] > C.hi[r] ? 2 : (zn[r] < C.lo[r] ? 1 : 0);
+        diff = diff || (c2 != cd[r]);
+      }
+      T.end(2);
+      if (wave_any(!isfinite(xn))) {
+        bad = true;
+        break;
+      }
+      if (!wave_any(diff)) {
+        x = xn;
+        pol_ok = true;
+        break;
+      }
+      // Armijo backtracking on the scaled objective along d = xn - x
+      T.begin();
+      const double dx = act ? xn - x : 0.0;
+      const double Px = C.Pmul(x);
+      const double Pd = C.Pmul(dx);
+      double zd[3], gt[3];
+#pragma unroll
+      for (int r = 0; r < 3; ++r) {
+        zd[r] = zn[r] - zc[r];
+        const double res = zc[r] > C.hi[r] ? zc[r] - C.hi[r] : (zc[r] < C.lo[r] ? zc[r] - C.lo[r] : 0.0);
+        gt[r] = 2.0 * C.wb[r] * res;
+      }
+      const double gr = C.CTmul(gt);
+      const double slope = wave_sum(act ? (Px + C.qv + gr) * dx : 0.0);
+      const double qd = wave_sum(act ? dx * Pd : 0.0);
+      const double lin = wave_sum(act ? (Px + C.qv) * dx : 0.0);
+      const double q0 = wave_sum(act ? x * (0.5 * Px + C.qv) : 0.0);
+      auto pen = [&](double t) -> double {
+        double s = 0.0;
+#pragma unroll
+        for (int r = 0; r < 3; ++r) {
+          const double zt = zc[r] + t * zd[r];
+          const double d = zt > C.hi[r] ? zt - C.hi[r] : (zt < C.lo[r] ? C.lo[r] - zt : 0.0);
+          s += C.wb[r] * d * d;
+        }
+        return wave_sum(s);
+      };
+      const double f0 = q0 + pen(0.0);
+      double t = 1.0;
+      for (int ls = 0; ls < 60; ++ls) {
+        ++n_ls;
+        const double ft = q0 + t * lin + 0.5 * t * t * qd + pen(t);
+        if (ft <= f0 + 1e-4 * t * slope) break;
+        t *= 0.5;
+      }
+      x = x + t * dx;
+      C.Cmul(x, zc);
+#pragma unroll
+      for (int r = 0; r < 3; ++r) cd[r] = zc[r] > C.hi[r] ? 2 : (zc[r] < C.lo[r] ? 1 : 0);
+      T.end(3);
+    }
+  }
+  T2.end(0);
+  T.flush(8);   // g_stamps[8..11]: polish form, sweep, solve+check, line search
+  T2.flush(12); // g_stamps[12]: polish phase of k_finish
+  if (wave_any(!isfinite(x))) bad = true;
+  int status;
+  if (bad) {
+    status = MPCQP_NUMERICAL_ERROR;
+  } else if (pol_ok) {
+    status = MPCQP_SOLVED;
+  } else if (use_admm) {
+    if (do_polish) x = x_admm;  // polish failed: return the ADMM iterate (OSQP behaviour)
+    status = admm_ok ? (do_polish ? MPCQP_SOLVED_INACCURATE : MPCQP_SOLVED) : MPCQP_MAX_ITER_REACHED;
+  } else {
+    status = MPCQP_MAX_ITER_REACHED;
+  }
+
+  // ---- outputs (unscaled) ----
+  const double* mb = model + (size_t)b * model_stride(N);
+  const int cc = lane & 1;
+  const double U = act ? C.D * x : 0.0;
+  const double dt = p.dt;
+  const double x00 = mb[11 * N + 4], x01 = mb[11 * N + 5], x02 = mb[11 * N + 6], x03 = mb[11 * N + 7];
+  const double up0 = mb[11 * N + 8], up1 = mb[11 * N + 9];
+  const double sj = act ? mb[4 * N + (lane >> 1)] : 0.0;
+  // v_{j+1} on lane 2j, psi_{j+1} on lane 2j+1
+  const double vacc = scan_add(C.even ? U : 0.0, lane);
+  const double sacc = scan_add((act && cc == 1) ? sj * U : 0.0, lane);
+  // lane k <- (psi_k, v_k)
+  const int srcv = lane == 0 ? 0 : 2 * (lane - 1);
+  const double vk_s = __shfl(vacc, srcv < kWave ? srcv : 0, kWave);
+  const double pk_s = __shfl(sacc, (srcv + 1) < kWave ? srcv + 1 : 0, kWave);
+  const double vk = lane == 0 ? x03 : x03 + dt * vk_s;
+  const double pk = lane == 0 ? x02 : x02 + pk_s;
+  double t0 = 0.0, t1 = 0.0;
+  if (lane < N) {
+    t0 = mb[lane] * pk + mb[N + lane] * vk + mb[5 * N + lane];
+    t1 = mb[2 * N + lane] * pk + mb[3 * N + lane] * vk + mb[6 * N + lane];
+  }
+  const double in0 = scan_add(t0, lane), in1 = scan_add(t1, lane);
+  const double ex0 = dpp<kWaveShr1>(in0), ex1 = dpp<kWaveShr1>(in1);  // exclusive prefix
+  const double Xk0 = x00 + ex0, Xk1 = x01 + ex1;
+  if (Xo && lane <= N) {
+    double* Xb = Xo + (size_t)b * 4 * (N + 1);
+    Xb[0 * (N + 1) + lane] = Xk0;
+    Xb[1 * (N + 1) + lane] = Xk1;
+    Xb[2 * (N + 1) + lane] = pk;
+    Xb[3 * (N + 1) + lane] = vk;
+  }
+  if (Uo && act) Uo[(size_t)b * n + cc * N + (lane >> 1)] = U;
+  if (u0o && lane < 2) u0o[(size_t)b * 2 + lane] = U;
+  const double Um2 = shr2(U);
+  if (activeo) {
+    uint8_t* ab = activeo + (size_t)b * (5 * N + 1);
+    if (lane <= N) ab[lane] = vk > p.v_bounds[1] ? 2 : (vk < p.v_bounds[0] ? 1 : 0);
+    if (act) {
+      ab[N + 1 + lane] = U > p.u_bounds[2 * cc + 1] ? 2 : (U < p.u_bounds[2 * cc] ? 1 : 0);
+      const double d = U - (lane < 2 ? (cc ? up1 : up0) : Um2);
+      ab[3 * N + 1 + lane] = d > p.du_bounds[2 * cc + 1] ? 2 : (d < p.du_bounds[2 * cc] ? 1 : 0);
+    }
+  }
+  if (lane == 0) {
+    statuso[b] = status;
+    if (iterso) {
+      iterso[4 * (size_t)b + 0] = admm_it;
+      iterso[4 * (size_t)b + 1] = pol_it;
+      iterso[4 * (size_t)b + 2] = nfact;
+      iterso[4 * (size_t)b + 3] = n_ls;
+    }
+  }
+}
+
+}  // namespace
+
+namespace mpcqp {
+template <int N>
+void launch_solve(hipStream_t s, const Launch& L) {
+  hipLaunchKernelGGL(k_setup<N>, dim3(L.B), dim3(kWave), 0, s, *L.p, L.B, L.model, L.state);
+  if (L.p->method == MPCQP_METHOD_ADMM) hipLaunchKernelGGL(k_admm<N>, dim3(L.B), dim3(kWave), 0, s, *L.p, L.B, L.state);
+  hipLaunchKernelGGL(k_finish<N>, dim3(L.B), dim3(kWave), 0, s, *L.p, L.B, L.model, L.state, L.u0, L.X, L.U, L.st,
+                     L.it, L.ac);
+}
+
+}  // namespace mpcqp
