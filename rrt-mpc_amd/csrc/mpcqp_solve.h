@@ -531,47 +531,45 @@ __global__ __launch_bounds__(kWave) void k_admm(mpcqp_params p, int B, double* _
       T.end(2);
       if (it % p.check_termination == 0 || it == p.max_iter) {
         T.begin();
+        // Residual norms (OSQP: unscaled for termination, scaled for the rho update).  The
+        // lane maxima are combined before the wave reductions (max distributes), which keeps
+        // the check's live set small.
         double Ax[3];
         C.Cmul(x, Ax);
-        const double Px = C.Pmul(x);
-        const double Aty = C.CTmul(y);
-        double pr = 0, nAx = 0, nz = 0, spr = 0, snAx = 0, snz = 0;
+        double pr = 0, nprim = 0, spr = 0, snprim = 0;
 #pragma unroll
         for (int r = 0; r < 3; ++r) {
           if (C.E[r] > 0.0) {
             const double ie = 1.0 / C.E[r];
             pr = fmax(pr, fabs((Ax[r] - z[r]) * ie));
-            nAx = fmax(nAx, fabs(Ax[r] * ie));
-            nz = fmax(nz, fabs(z[r] * ie));
+            nprim = fmax(nprim, fmax(fabs(Ax[r] * ie), fabs(z[r] * ie)));
             spr = fmax(spr, fabs(Ax[r] - z[r]));
-            snAx = fmax(snAx, fabs(Ax[r]));
-            snz = fmax(snz, fabs(z[r]));
+            snprim = fmax(snprim, fmax(fabs(Ax[r]), fabs(z[r])));
           }
         }
-        double du = 0, nPx = 0, nAty = 0, nq = 0, sdu = 0, snPx = 0, snAty = 0, snq = 0;
+        pr = wave_max(pr);
+        nprim = wave_max(nprim);
+        spr = wave_max(spr);
+        snprim = wave_max(snprim);
+        const double Px = C.Pmul(x);
+        const double Aty = C.CTmul(y);
+        double du = 0, ndual = 0, sdu = 0, sndual = 0;
         if (act) {
           const double id = 1.0 / C.D;
           const double rd = Px + C.qv + Aty;
           du = fabs(rd * id);
-          nPx = fabs(Px * id);
-          nAty = fabs(Aty * id);
-          nq = fabs(C.qv * id);
+          ndual = fmax(fmax(fabs(Px * id), fabs(Aty * id)), fabs(C.qv * id));
           sdu = fabs(rd);
-          snPx = fabs(Px);
-          snAty = fabs(Aty);
-          snq = fabs(C.qv);
+          sndual = fmax(fmax(fabs(Px), fabs(Aty)), fabs(C.qv));
         }
-        pr = wave_max(pr);
-        nAx = wave_max(nAx);
-        nz = wave_max(nz);
         du = wave_max(du);
-        nPx = wave_max(nPx);
-        nAty = wave_max(nAty);
-        nq = wave_max(nq);
+        ndual = wave_max(ndual);
+        sdu = wave_max(sdu);
+        sndual = wave_max(sndual);
         const double ic = 1.0 / C.cscale;
         du *= ic;
-        const double ep = p.eps_abs + p.eps_rel * fmax(nAx, nz);
-        const double ed = p.eps_abs + p.eps_rel * fmax(fmax(nPx, nAty), nq) * ic;
+        const double ep = p.eps_abs + p.eps_rel * nprim;
+        const double ed = p.eps_abs + p.eps_rel * ndual * ic;
         T.end(3);
         // fmax drops NaNs, so test the iterate itself
         if (wave_any(!isfinite(x) || !isfinite(z[0] + z[1] + z[2]) || !isfinite(y[0] + y[1] + y[2])) ||
@@ -584,15 +582,8 @@ __global__ __launch_bounds__(kWave) void k_admm(mpcqp_params p, int B, double* _
           break;
         }
         if (p.adaptive_rho && it % p.adaptive_rho_interval == 0) {
-          spr = wave_max(spr);
-          snAx = wave_max(snAx);
-          snz = wave_max(snz);
-          sdu = wave_max(sdu);
-          snPx = wave_max(snPx);
-          snAty = wave_max(snAty);
-          snq = wave_max(snq);
-          const double pn = spr / (fmax(snAx, snz) + kDivTol);
-          const double dn = sdu / (fmax(fmax(snPx, snAty), snq) + kDivTol);
+          const double pn = spr / (snprim + kDivTol);
+          const double dn = sdu / (sndual + kDivTol);
           double rn = rho * sqrt(pn / (dn + kDivTol));
           rn = fmin(fmax(rn, kRhoMin), kRhoMax);
           if (rn > rho * p.adaptive_rho_tolerance || rn < rho / p.adaptive_rho_tolerance) {
