@@ -1,7 +1,15 @@
+# One GPU call: parity tests, smoke, bench, kernel-trace profile, two PMC passes (HBM bytes).
+# usage: gpurun --timeout 1100 -- 'bash tools/gpu_round.sh'
 set -o pipefail
 R=$GRAFT_REPO_ROOT
-timeout -k 10 400 python -m pytest tests -m gpu -x -q > gpurun_out/pytest_gpu.log 2>&1 &&
-timeout -k 10 200 python tools/phase_timing.py > gpurun_out/phase.json 2>&1 &&
-timeout -k 10 300 python bench.py > gpurun_out/bench.json 2> gpurun_out/bench.err &&
+O=$R/gpurun_out
+mkdir -p $O
+timeout -k 10 400 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > $O/pytest_gpu.log 2>&1 &&
+timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 &&
+timeout -k 10 300 python bench.py > $O/bench.json 2> $O/bench.err &&
 cd /tmp && export TMPDIR=/tmp &&
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/prof -o run -f csv -- python3 $R/bench.py --steps 10 --warmup 2 > $R/gpurun_out/bench_prof.json 2> $R/gpurun_out/bench_prof.err
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof -o run -f csv -- python3 $R/bench.py --steps 10 --warmup 2 --cpu-seconds 0 > $O/bench_prof.json 2> $O/bench_prof.err &&
+timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -d $O/pmc_fetch -o run -f csv -- python3 $R/bench.py --steps 3 --warmup 1 --cpu-seconds 0 > $O/pmc_fetch.log 2>&1 &&
+timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE -d $O/pmc_write -o run -f csv -- python3 $R/bench.py --steps 3 --warmup 1 --cpu-seconds 0 > $O/pmc_write.log 2>&1 &&
+timeout -s KILL 120 rocprofv3 --pmc TCC_EA0_RDREQ_sum TCC_EA0_WRREQ_sum -d $O/pmc_req -o run -f csv -- python3 $R/bench.py --steps 3 --warmup 1 --cpu-seconds 0 > $O/pmc_req.log 2>&1
+echo "exit $?"
