@@ -1,0 +1,77 @@
+#!/usr/bin/env python3
+"""Fold rocprofv3 --pmc passes (FETCH_SIZE, WRITE_SIZE, TCC_EA0_*REQ) into profiles/pmc_traffic.json.
+
+    python tools/pmc_traffic.py gpurun_out --N 20 --B 4096 > profiles/pmc_traffic.json
+
+Units and corrections (MI355X_MICROARCH.md, HBM section):
+  * FETCH_SIZE / WRITE_SIZE are in KiB (FETCH_SIZE = TCC_EA0_RDREQ x 64 B / 1024, checked
+    against the TCC_EA0_RDREQ_sum pass);
+  * gfx950 FETCH_SIZE reports 1/2 of the bytes of wide streaming reads: the read side is
+    doubled (an upper bound for this kernel's 8-byte-per-lane reads; k_build, whose read
+    bytes are known exactly, calibrates that access width and is reported beside it);
+  * WRITE_SIZE is taken as is.
+k_solve = k_setup + k_admm + k_finish (one mpcqp_solve call).
+"""
+from __future__ import annotations
+
+import argparse
+import collections
+import csv
+import json
+from pathlib import Path
+
+SOLVE = ("k_setup", "k_admm", "k_finish")
+
+
+def per_kernel(path: Path) -> dict:
+    acc = collections.defaultdict(list)
+    for r in csv.DictReader(open(path)):
+        name = r["Kernel_Name"]
+        short = next((k for k in (*SOLVE, "k_build") if k in name), None)
+        if short:
+            acc[(short, r["Counter_Name"])].append(float(r["Counter_Value"]))
+    return {k: sum(v) / len(v) for k, v in acc.items()}
+
+
+def main() -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("out_dir")
+    ap.add_argument("--N", type=int, default=20)
+    ap.add_argument("--B", type=int, default=4096)
+    a = ap.parse_args()
+    d = Path(a.out_dir)
+    c = {}
+    for p in ("pmc_fetch", "pmc_write", "pmc_req"):
+        f = d / p / "run_counter_collection.csv"
+        if f.exists():
+            c.update(per_kernel(f))
+    kib = 1024.0
+    fetch = {k: c[(k, "FETCH_SIZE")] * kib for k in (*SOLVE, "k_build")}
+    write = {k: c[(k, "WRITE_SIZE")] * kib for k in (*SOLVE, "k_build")}
+    rdreq = {k: c.get((k, "TCC_EA0_RDREQ_sum")) for k in (*SOLVE, "k_build")}
+    N, B = a.N, a.B
+    build_read_alg = 8.0 * B * (4 * (N + 1) + 6)
+    read = 2.0 * sum(fetch[k] for k in SOLVE)
+    wr = sum(write[k] for k in SOLVE)
+    out = {
+        f"N{N}_B{B}": {
+            "k_solve_hbm_bytes_per_launch": read + wr,
+            "k_solve_read_bytes_corrected": read,
+            "k_solve_write_bytes": wr,
+            "per_kernel_fetch_bytes_raw": fetch,
+            "per_kernel_write_bytes": write,
+            "per_kernel_tcc_ea0_rdreq": rdreq,
+            "k_build_read_calibration": {"algorithmic_read_bytes": build_read_alg,
+                                          "fetch_bytes_raw": fetch["k_build"],
+                                          "ratio": build_read_alg / fetch["k_build"]},
+            "per_qp_bytes": (read + wr) / B,
+            "note": "FETCH doubled per the gfx950 correction; the solver's per-QP state (scaled "
+                    "Hessian etc., written by k_setup, re-read by k_admm and k_finish) dominates and "
+                    "stays Infinity-Cache resident, which these fabric-side counters still count",
+        }
+    }
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main()
