@@ -144,6 +144,53 @@ int mpcqp_build(mpcqp_ws* ws, int B, const double* x0, const double* ref, const 
 int mpcqp_solve(mpcqp_ws* ws, int B, double* u0, double* X, double* U, int32_t* status,
                 int32_t* iters, uint8_t* active, void* stream);
 
+/*
+ * Closed-loop fleet: V vehicles tracking their own references, one MPC step each per call
+ * (SURVEY.md §8f row 1).  Replaces, per vehicle, one iteration of the loop body of
+ * TrajectoryTracker.track (src/pipeline/control_stage.py:100-150):
+ *   window gather + tail padding (:101-105), _solve_with_relaxation (:33-56, :107-110),
+ *   plant f_discrete (:127, vehicle_model.py:11-21), u_prev (:129), path_idx advance
+ *   (:141-145), goal test (:147-150).
+ * Every pointer is caller-owned DEVICE memory; the per-vehicle loop state lives on the
+ * device between calls, so a run of steps needs no host round trip.
+ */
+#define MPCQP_FLEET_RUNNING 0
+#define MPCQP_FLEET_GOAL 1        /* hypot(state - goal) < 8 after a step (control_stage.py:147) */
+#define MPCQP_FLEET_ABORTED 2     /* unsolved after relaxation (control_stage.py:108-110) */
+#define MPCQP_FLEET_OUT_OF_STEPS 3 /* steps == max_steps (sim_steps) */
+
+typedef struct mpcqp_fleet {
+  int32_t vehicles;          /* V (<= max_batch of both workspaces) */
+  int32_t ref_stride;        /* rows per vehicle in ref_global */
+  int32_t max_steps;         /* sim_steps: rows per vehicle in trace / u_trace */
+  int32_t reserved;
+  const double* ref_global;  /* V x ref_stride x 4: build_reference() output, rows >= ref_len unused */
+  const int32_t* ref_len;    /* V: valid rows, >= 1 */
+  const double* goal;        /* V x 2 */
+  double* state;             /* V x 4 (in/out) */
+  double* u_prev;            /* V x 2 (in/out) */
+  int32_t* path_idx;         /* V (in/out) */
+  int32_t* phase;            /* V (in/out): MPCQP_FLEET_* */
+  int32_t* steps;            /* V (in/out): closed-loop steps taken = rows written to trace */
+  uint8_t* mask;             /* 2 x V scratch: solve-this-QP masks (nominal, relaxed) */
+  int32_t* status;           /* 2 x V out: status of the nominal / relaxed solve of the last step */
+  double* u0;                /* 2 x V x 2 out: u0 of the nominal / relaxed solve of the last step */
+  double* X;                 /* V x 4 x (N+1) out: prediction of the accepted solve (nullable) */
+  double* trace;             /* V x max_steps x 4: state after each step, TrackingResult.states (nullable) */
+  double* u_trace;           /* V x max_steps x 2: applied input of each step (nullable) */
+} mpcqp_fleet;
+
+/* One closed-loop step for every RUNNING vehicle.  `nominal` holds the base parameters,
+ * `relaxed` the retry parameters of control_stage.py:45-55 (du_bounds widened by
+ * (5, 0.05); the reference speed column is scaled by 0.6 on the device); both have the
+ * same horizon and max_batch >= V.  Vehicles not RUNNING are skipped (their waves exit). */
+int mpcqp_fleet_step(mpcqp_ws* nominal, mpcqp_ws* relaxed, const mpcqp_fleet* f, void* stream);
+
+/* `steps` calls of mpcqp_fleet_step.  use_graph != 0 captures one step in a hipGraph on an
+ * internal stream (ordered after / before `stream` by events) and replays it `steps` times. */
+int mpcqp_fleet_run(mpcqp_ws* nominal, mpcqp_ws* relaxed, const mpcqp_fleet* f, int steps, int use_graph,
+                    void* stream);
+
 /* Workspace device buffers (for tests / inspection), layouts documented in DESIGN.md:
  *   model: K1 output, B x mpcqp_model_stride(N) doubles
  *   state: scaled QP + ADMM iterate (K2a/K2b output), B x mpcqp_state_stride(N) doubles */

@@ -13,7 +13,7 @@
 // its own register budget (occupancy); the per-QP solver state between them
 // (scaled Hessian + scaling vectors, ~20 KB at N=20) stays L2/MALL resident.
 // The algorithm is restated sequentially in oracle/mpcqp_cpu.c -- see DESIGN.md.
-#include "mpcqp_common.h"
+#include "mpcqp_build.h"
 #ifdef MPCQP_ONLY_N
 #include "mpcqp_solve.h"  // development builds: one horizon, one translation unit
 #endif
@@ -22,11 +22,8 @@ namespace {
 using mpcqp::Launch;
 
 // ------------------------------------------------------------------ K1: build
-// Per QP (one wave, lane k = horizon step k in [0, N]):
-//   unwrapped yaw (np.unwrap, mpc_controller.py:60), then linearize() at
-//   ref[max(k-1,0)], u = 0 (mpc_controller.py:65-70,108; vehicle_model.py:24-45).
-// Model layout per QP (doubles): alpha[N] beta[N] gamma[N] eta[N] sigma[N] c0[N]
-// c1[N] ref[(N+1)*4] x0[4] u_prev[2], stride model_stride(N).
+// Per QP (one wave, lane k = horizon step k in [0, N]) on caller-provided windows; the body
+// (unwrap + linearize) is build_qp in mpcqp_build.h.
 __global__ __launch_bounds__(kWave) void k_build(mpcqp_params p, int B, const double* __restrict__ x0,
                                                  const double* __restrict__ ref,
                                                  const double* __restrict__ u_prev,
@@ -35,9 +32,7 @@ __global__ __launch_bounds__(kWave) void k_build(mpcqp_params p, int B, const do
   const int lane = threadIdx.x;
   if (b >= B) return;
   const int N = p.horizon;
-  const int S = model_stride(N);
   const double* rb = ref + (size_t)b * (N + 1) * 4;
-  double* mb = model + (size_t)b * S;
   double rx = 0.0, ry = 0.0, ryaw = 0.0, rv = 0.0;
   if (lane <= N) {
     rx = rb[4 * lane + 0];
@@ -45,60 +40,11 @@ __global__ __launch_bounds__(kWave) void k_build(mpcqp_params p, int B, const do
     ryaw = rb[4 * lane + 2];
     rv = rb[4 * lane + 3];
   }
-  // np.unwrap: ddmod = mod(dd + pi, 2pi) - pi; boundary fix; zero when |dd| < pi
-  const double prev = dpp<kWaveShr1>(ryaw);
-  double pc = 0.0;
-  if (lane >= 1 && lane <= N) {
-    const double dd = ryaw - prev;
-    double ddmod = np_mod(dd + kPi, kTwoPi) + (-kPi);
-    if (ddmod == -kPi && dd > 0.0) ddmod = kPi;
-    pc = ddmod - dd;
-    if (fabs(dd) < kPi) pc = 0.0;
-  }
-  // cumsum in numpy's sequential order (bit-exact)
-  double cs = 0.0, mine = 0.0;
-  for (int j = 1; j <= N; ++j) {
-    cs = cs + readlane(pc, j);
-    if (lane == j) mine = cs;
-  }
-  const double uyaw = lane == 0 ? ryaw : ryaw + mine;
-  if (lane <= N) {
-    mb[7 * N + 4 * lane + 0] = rx;
-    mb[7 * N + 4 * lane + 1] = ry;
-    mb[7 * N + 4 * lane + 2] = uyaw;
-    mb[7 * N + 4 * lane + 3] = rv;
-  }
-  // linearisation point of step k: ref[max(k-1, 0)]
-  // (DPP must run with every lane active: an exec-masked source lane reads as 0)
-  const double psi_m1 = dpp<kWaveShr1>(uyaw);
-  const double v_m1 = dpp<kWaveShr1>(rv);
-  const double psi = lane == 0 ? uyaw : psi_m1;
-  const double v = lane == 0 ? rv : v_m1;
-  if (lane < N) {
-    const double dt = p.dt, L = p.wheelbase_px;
-    const double sec2 = 1.0 / (1.0 * 1.0 + 1e-9);
-    double s, c;
-    sincos(psi, &s, &c);
-    const double al = -dt * v * s;
-    const double ga = dt * v * c;
-    mb[lane] = al;
-    mb[N + lane] = dt * c;
-    mb[2 * N + lane] = ga;
-    mb[3 * N + lane] = dt * s;
-    mb[4 * N + lane] = dt * (v / L) * sec2;
-    mb[5 * N + lane] = -al * psi;
-    mb[6 * N + lane] = -ga * psi;
-  }
-  if (lane < 4) mb[11 * N + 4 + lane] = x0[(size_t)b * 4 + lane];
-  if (lane >= 4 && lane < 6) mb[11 * N + 4 + lane] = u_prev ? u_prev[(size_t)b * 2 + lane - 4] : 0.0;
+  const double x0l = lane < 4 ? x0[(size_t)b * 4 + lane] : 0.0;
+  const double upl = (lane >= 4 && lane < 6 && u_prev) ? u_prev[(size_t)b * 2 + lane - 4] : 0.0;
+  build_qp(p, lane, rx, ry, ryaw, rv, x0l, upl, model + (size_t)b * model_stride(N));
 }
 
-// ------------------------------------------------------------------ K2a: setup
-// Condensing (states and slacks eliminated) + OSQP Ruiz/cost scaling.
-// Row slots owned by lane p (p < n = 2N):
-//   slot 0: v row (p even): v_{p/2+1} - v0 = dt * sum_{j<=p/2} a_j   (mpc_controller.py:81-82,115-116)
-//   slot 1: input row        U_p                                      (:83-86)
-//   slot 2: rate row         U_p - U_{p-2} (u_prev at k = 0)          (:89-106)
 // ------------------------------------------------------------------ test hook: wave primitives
 // out[op][lane] for the 64-lane input `in` (tests/test_gpu_parity.py checks them with numpy).
 __global__ __launch_bounds__(kWave) void k_wave_ops(const double* __restrict__ in, double* __restrict__ out) {
@@ -130,11 +76,7 @@ const mpcqp::launcher_t kLaunchers[MPCQP_MAX_HORIZON + 1] = {
 #undef MPCQP_L
 
 thread_local std::string g_err;
-
-int fail(int code, const std::string& msg) {
-  g_err = msg;
-  return code;
-}
+using mpcqp::fail;
 
 int check_params(const mpcqp_params* p) {
   if (!p) return fail(MPCQP_E_ARG, "null params");
@@ -153,14 +95,15 @@ int check_params(const mpcqp_params* p) {
 
 }  // namespace
 
-struct mpcqp_ws {
-  mpcqp_params p;
-  int max_batch;
-  int device;
-  int built_B;
-  double* model;
-  double* state;
-};
+namespace mpcqp {
+int fail(int code, const std::string& msg) {
+  g_err = msg;
+  return code;
+}
+launcher_t launcher(int horizon) {
+  return horizon >= 1 && horizon <= MPCQP_MAX_HORIZON ? kLaunchers[horizon] : nullptr;
+}
+}  // namespace mpcqp
 
 extern "C" {
 
@@ -237,7 +180,7 @@ int mpcqp_solve(mpcqp_ws* ws, int B, double* u0, double* X, double* U, int32_t* 
   if (B != ws->built_B) return fail(MPCQP_E_STATE, "mpcqp_solve B differs from the last mpcqp_build");
   if (B == 0) return MPCQP_OK;
   hipStream_t s = static_cast<hipStream_t>(stream);
-  Launch L{&ws->p, B, ws->model, ws->state, u0, X, U, status, iters, active};
+  Launch L{&ws->p, B, ws->model, ws->state, u0, X, U, status, iters, active, nullptr};
   kLaunchers[ws->p.horizon](s, L);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return fail(MPCQP_E_HIP, std::string("k_solve launch: ") + hipGetErrorString(e));

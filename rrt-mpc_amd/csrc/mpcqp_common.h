@@ -248,6 +248,7 @@ struct Launch {
   double *u0, *X, *U;
   int32_t *st, *it;
   uint8_t* ac;
+  const uint8_t* mask;  // QP b is solved iff mask == nullptr or mask[b] != 0 (fleet steps)
 };
 
 typedef void (*launcher_t)(hipStream_t, const Launch&);
@@ -255,4 +256,18 @@ typedef void (*launcher_t)(hipStream_t, const Launch&);
 // mpcqp_part.hip objects (parallel build) or in mpcqp.hip itself (MPCQP_ONLY_N dev builds).
 template <int N>
 void launch_solve(hipStream_t s, const Launch& L);
+// launcher of horizon N (nullptr when not compiled in); defined in mpcqp.hip
+launcher_t launcher(int horizon);
+// records msg as mpcqp_last_error() of the calling thread and returns code; defined in mpcqp.hip
+int fail(int code, const std::string& msg);
 }  // namespace mpcqp
+
+// Workspace of one device: parameter block + per-QP model (K1 output) and solver state.
+struct mpcqp_ws {
+  mpcqp_params p;
+  int max_batch;
+  int device;
+  int built_B;
+  double* model;
+  double* state;
+};

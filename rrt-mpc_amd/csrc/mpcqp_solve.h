@@ -18,15 +18,15 @@ struct SetupSmem {
 };
 
 template <int N>
-__global__ __launch_bounds__(kWave) void k_setup(mpcqp_params p, int B, const double* __restrict__ model,
-                                                 double* __restrict__ state) {
+__global__ __launch_bounds__(kWave) void k_setup(mpcqp_params p, int B, const uint8_t* __restrict__ mask,
+                                                 const double* __restrict__ model, double* __restrict__ state) {
   constexpr int n = 2 * N;
   constexpr int LD = SetupSmem<N>::LD;
   constexpr int S = model_stride(N);
   __shared__ SetupSmem<N> sm;
   const int b = blockIdx.x;
   const int lane = threadIdx.x;
-  if (b >= B) return;
+  if (b >= B || (mask && !mask[b])) return;
   const bool act = lane < n;
   const bool even = act && ((lane & 1) == 0);
   const int cc = lane & 1;  // 0 = acceleration, 1 = steering
@@ -465,10 +465,11 @@ struct SolveSmem {
 
 // ------------------------------------------------------------------ K2b: ADMM
 template <int N>
-__global__ __launch_bounds__(kWave) void k_admm(mpcqp_params p, int B, double* __restrict__ state) {
+__global__ __launch_bounds__(kWave) void k_admm(mpcqp_params p, int B, const uint8_t* __restrict__ mask,
+                                                double* __restrict__ state) {
   __shared__ SolveSmem<N> sm;
   const int b = blockIdx.x;
-  if (b >= B) return;
+  if (b >= B || (mask && !mask[b])) return;
   double* st = state + (size_t)b * state_stride(N);
   Ctx<N> C;
   C.load(st, threadIdx.x, p.dt, sm.buf, sm.sv, sm.Dl, sm.P);
@@ -609,7 +610,8 @@ __global__ __launch_bounds__(kWave) void k_admm(mpcqp_params p, int B, double* _
 
 // ------------------------------------------------------------------ K2c: polish + outputs
 template <int N>
-__global__ __launch_bounds__(kWave) void k_finish(mpcqp_params p, int B, const double* __restrict__ model,
+__global__ __launch_bounds__(kWave) void k_finish(mpcqp_params p, int B, const uint8_t* __restrict__ mask,
+                                                  const double* __restrict__ model,
                                                   const double* __restrict__ state, double* __restrict__ u0o,
                                                   double* __restrict__ Xo, double* __restrict__ Uo,
                                                   int32_t* __restrict__ statuso, int32_t* __restrict__ iterso,
@@ -617,7 +619,7 @@ __global__ __launch_bounds__(kWave) void k_finish(mpcqp_params p, int B, const d
   constexpr int n = 2 * N;
   __shared__ SolveSmem<N> sm;
   const int b = blockIdx.x;
-  if (b >= B) return;
+  if (b >= B || (mask && !mask[b])) return;
   const int lane = threadIdx.x;
   const double* st = state + (size_t)b * state_stride(N);
   Ctx<N> C;
@@ -843,10 +845,11 @@ __global__ __launch_bounds__(kWave) void k_finish(mpcqp_params p, int B, const d
 namespace mpcqp {
 template <int N>
 void launch_solve(hipStream_t s, const Launch& L) {
-  hipLaunchKernelGGL(k_setup<N>, dim3(L.B), dim3(kWave), 0, s, *L.p, L.B, L.model, L.state);
-  if (L.p->method == MPCQP_METHOD_ADMM) hipLaunchKernelGGL(k_admm<N>, dim3(L.B), dim3(kWave), 0, s, *L.p, L.B, L.state);
-  hipLaunchKernelGGL(k_finish<N>, dim3(L.B), dim3(kWave), 0, s, *L.p, L.B, L.model, L.state, L.u0, L.X, L.U, L.st,
-                     L.it, L.ac);
+  hipLaunchKernelGGL(k_setup<N>, dim3(L.B), dim3(kWave), 0, s, *L.p, L.B, L.mask, L.model, L.state);
+  if (L.p->method == MPCQP_METHOD_ADMM)
+    hipLaunchKernelGGL(k_admm<N>, dim3(L.B), dim3(kWave), 0, s, *L.p, L.B, L.mask, L.state);
+  hipLaunchKernelGGL(k_finish<N>, dim3(L.B), dim3(kWave), 0, s, *L.p, L.B, L.mask, L.model, L.state, L.u0, L.X, L.U,
+                     L.st, L.it, L.ac);
 }
 
 }  // namespace mpcqp

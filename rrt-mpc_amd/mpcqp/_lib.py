@@ -107,6 +107,37 @@ def to_c_params(params, method: int = METHOD_ADMM, **settings) -> MpcqpParams:
     return c
 
 
+FLEET_RUNNING = 0
+FLEET_GOAL = 1
+FLEET_ABORTED = 2
+FLEET_OUT_OF_STEPS = 3
+
+
+class MpcqpFleet(ctypes.Structure):
+    """``mpcqp_fleet`` (include/mpcqp.h): device pointers of the closed-loop fleet state."""
+
+    _fields_ = [
+        ("vehicles", ctypes.c_int32),
+        ("ref_stride", ctypes.c_int32),
+        ("max_steps", ctypes.c_int32),
+        ("reserved", ctypes.c_int32),
+        ("ref_global", ctypes.c_void_p),
+        ("ref_len", ctypes.c_void_p),
+        ("goal", ctypes.c_void_p),
+        ("state", ctypes.c_void_p),
+        ("u_prev", ctypes.c_void_p),
+        ("path_idx", ctypes.c_void_p),
+        ("phase", ctypes.c_void_p),
+        ("steps", ctypes.c_void_p),
+        ("mask", ctypes.c_void_p),
+        ("status", ctypes.c_void_p),
+        ("u0", ctypes.c_void_p),
+        ("X", ctypes.c_void_p),
+        ("trace", ctypes.c_void_p),
+        ("u_trace", ctypes.c_void_p),
+    ]
+
+
 class LibraryError(RuntimeError):
     pass
 
@@ -124,6 +155,10 @@ _SYMBOLS = {
     "mpcqp_build": ([ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                      ctypes.c_void_p], ctypes.c_int),
     "mpcqp_solve": ([ctypes.c_void_p, ctypes.c_int] + [ctypes.c_void_p] * 7, ctypes.c_int),
+    "mpcqp_fleet_step": ([ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(MpcqpFleet), ctypes.c_void_p],
+                         ctypes.c_int),
+    "mpcqp_fleet_run": ([ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(MpcqpFleet), ctypes.c_int, ctypes.c_int,
+                         ctypes.c_void_p], ctypes.c_int),
     "mpcqp_model_buffer": ([ctypes.c_void_p], ctypes.c_void_p),
     "mpcqp_model_stride": ([ctypes.c_int], ctypes.c_int),
     "mpcqp_state_buffer": ([ctypes.c_void_p], ctypes.c_void_p),
@@ -166,7 +201,12 @@ def check(rc: int, what: str) -> None:
 
 __all__ = [
     "MpcqpParams",
+    "MpcqpFleet",
     "to_c_params",
+    "FLEET_RUNNING",
+    "FLEET_GOAL",
+    "FLEET_ABORTED",
+    "FLEET_OUT_OF_STEPS",
     "lib",
     "check",
     "LibraryError",

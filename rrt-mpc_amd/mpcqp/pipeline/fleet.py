@@ -1,0 +1,213 @@
+"""Closed-loop tracking for a fleet of vehicles, resident on the GPU.
+
+``FleetTracker`` runs the loop body of the reference's ``TrajectoryTracker.track``
+(``src/pipeline/control_stage.py:100-150``) for V vehicles at once through
+``mpcqp_fleet_run`` (``csrc/mpcqp_fleet.hip``): per step, a masked batched MPC solve
+with the reference's relaxation retry (``:33-56``), the plant ``f_discrete`` (``:127``),
+the ``path_idx`` advance (``:141-145``) and the goal test (``:147-150``), all on the
+device.  The host only checks every ``check_every`` steps whether any vehicle still runs.
+
+Each vehicle follows exactly the reference's single-vehicle semantics, so vehicle ``v``
+reproduces ``TrajectoryTracker.track`` on its own plan (tests/test_gpu_fleet.py).
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass, replace
+from typing import List, Optional, Sequence
+
+import numpy as np
+
+from .. import _lib
+from ..control.ref_builder import build_reference
+from .control_stage import TrackingResult
+
+PHASE_NAMES = {
+    _lib.FLEET_RUNNING: "running",
+    _lib.FLEET_GOAL: "goal_reached",
+    _lib.FLEET_ABORTED: "aborted",
+    _lib.FLEET_OUT_OF_STEPS: "out_of_steps",
+}
+
+
+def relaxed_parameters(base_params):
+    """The retry parameters of ``control_stage.py:50-56`` (du_bounds widened by (5, 0.05))."""
+    return replace(
+        base_params,
+        du_bounds=(
+            (base_params.du_bounds[0][0] - 5.0, base_params.du_bounds[0][1] + 5.0),
+            (base_params.du_bounds[1][0] - 0.05, base_params.du_bounds[1][1] + 0.05),
+        ),
+    )
+
+
+def initial_state(path: Sequence, start) -> np.ndarray:
+    """``control_stage.py:74-79``: start position, heading of the first path segment, 5 px/s."""
+    if len(path) > 1:
+        yaw0 = float(np.arctan2(path[1][1] - path[0][1], path[1][0] - path[0][0]))
+    else:
+        yaw0 = 0.0
+    return np.array([start[0], start[1], yaw0, 5.0], dtype=float)
+
+
+@dataclass
+class FleetResult:
+    """Per-vehicle outcome of a fleet run (host copies)."""
+
+    states: List[np.ndarray]  # vehicle v: (steps[v], 4) states after each step (TrackingResult.states)
+    inputs: List[np.ndarray]  # vehicle v: (steps[v], 2) applied u0
+    phase: np.ndarray  # (V,) int32: 0 running, 1 goal reached, 2 aborted, 3 out of steps
+    steps: np.ndarray  # (V,) int32
+    path_idx: np.ndarray  # (V,) int32
+
+    def tracking_results(self) -> List[TrackingResult]:
+        return [TrackingResult(states=[s.copy() for s in st]) for st in self.states]
+
+
+class FleetTracker:
+    """V vehicles in closed loop on one GPU; every loop step runs on the device.
+
+    ``mpc`` is an ``MPCConfig`` (reference or ``mpcqp.config``); the solver parameters
+    are ``mpc.to_parameters(map_resolution)`` as in ``control_stage.py:73``.
+    """
+
+    def __init__(self, mpc, *, map_resolution: float, max_vehicles: int, max_ref_len: int,
+                 device=None, use_graph: bool = True, **settings) -> None:
+        import torch
+
+        from ..control.mpc_controller import BatchedMPCController
+
+        self._torch = torch
+        self.mpc = mpc
+        self.params = mpc.to_parameters(map_resolution)
+        self.horizon = int(self.params.horizon)
+        self.max_vehicles = int(max_vehicles)
+        self.max_ref_len = int(max_ref_len)
+        self.use_graph = bool(use_graph)
+        self._nominal = BatchedMPCController(self.params, self.max_vehicles, device=device, **settings)
+        self._relaxed = BatchedMPCController(relaxed_parameters(self.params), self.max_vehicles,
+                                             device=self._nominal.device, **settings)
+        self.device = self._nominal.device
+        self._L = _lib.lib()
+        self._bufs = None
+        self._fleet = None
+        self.vehicles = 0
+
+    # ------------------------------------------------------------------
+    def reset(self, ref_globals: Sequence[np.ndarray], states0: np.ndarray, goals: np.ndarray,
+              max_steps: Optional[int] = None) -> None:
+        """Load V references (each ``(M_v, 4)``, ``build_reference`` output), start states and goals."""
+        torch = self._torch
+        V = len(ref_globals)
+        if V > self.max_vehicles:
+            raise ValueError(f"{V} vehicles exceed max_vehicles {self.max_vehicles}")
+        states0 = np.asarray(states0, dtype=float).reshape(V, 4)
+        goals = np.asarray(goals, dtype=float).reshape(V, 2)
+        max_steps = int(self.mpc.sim_steps if max_steps is None else max_steps)
+        if max_steps < 1:
+            raise ValueError("max_steps must be >= 1")
+        lens = np.array([len(r) for r in ref_globals], dtype=np.int32)
+        if V and (lens.min() < 1 or lens.max() > self.max_ref_len):
+            raise ValueError(f"reference lengths must be in [1, {self.max_ref_len}]")
+        M = self.max_ref_len
+        ref = np.zeros((max(V, 1), M, 4))
+        for v, r in enumerate(ref_globals):
+            r = np.asarray(r, dtype=float)
+            if r.ndim != 2 or r.shape[1] != 4:
+                raise ValueError("each reference must have shape (M, 4)")
+            ref[v, : len(r)] = r
+        N = self.horizon
+        dev = dict(device=self.device)
+        f64 = torch.float64
+        i32 = torch.int32
+        b = {
+            "ref_global": torch.from_numpy(ref).to(**dev),
+            "ref_len": torch.from_numpy(np.maximum(lens, 1) if V else np.ones(1, np.int32)).to(**dev),
+            "goal": torch.from_numpy(goals if V else np.zeros((1, 2))).to(**dev),
+            "state": torch.from_numpy(states0 if V else np.zeros((1, 4))).to(**dev),
+            "u_prev": torch.zeros((max(V, 1), 2), dtype=f64, **dev),
+            "path_idx": torch.zeros((max(V, 1),), dtype=i32, **dev),
+            "phase": torch.zeros((max(V, 1),), dtype=i32, **dev),
+            "steps": torch.zeros((max(V, 1),), dtype=i32, **dev),
+            "mask": torch.zeros((2, max(V, 1)), dtype=torch.uint8, **dev),
+            "status": torch.zeros((2, max(V, 1)), dtype=i32, **dev),
+            "u0": torch.zeros((2, max(V, 1), 2), dtype=f64, **dev),
+            "X": torch.zeros((max(V, 1), 4, N + 1), dtype=f64, **dev),
+            "trace": torch.zeros((max(V, 1), max_steps, 4), dtype=f64, **dev),
+            "u_trace": torch.zeros((max(V, 1), max_steps, 2), dtype=f64, **dev),
+        }
+        f = _lib.MpcqpFleet()
+        f.vehicles = V
+        f.ref_stride = M
+        f.max_steps = max_steps
+        for name, t in b.items():
+            setattr(f, name, t.data_ptr())
+        self._bufs = b
+        self._fleet = f
+        self.vehicles = V
+        self.max_steps = max_steps
+
+    def reset_from_plans(self, paths: Sequence, starts: np.ndarray, goals: np.ndarray,
+                         max_steps: Optional[int] = None) -> List[np.ndarray]:
+        """``control_stage.py:69-87`` per vehicle: references from the planned paths, start states."""
+        refs, states = [], []
+        for path, start in zip(paths, starts):
+            if not len(path):
+                raise RuntimeError("Planner returned an empty path")
+            refs.append(build_reference(path, self.mpc.v_px_s, self.horizon, self.mpc.dt))
+            states.append(initial_state(path, start))
+        self.reset(refs, np.array(states).reshape(-1, 4), goals, max_steps)
+        return refs
+
+    # ------------------------------------------------------------------
+    def step(self, steps: int = 1, stream=None) -> None:
+        """Enqueue ``steps`` closed-loop steps (asynchronous on the current torch stream)."""
+        if self._fleet is None:
+            raise RuntimeError("reset() the fleet first")
+        torch = self._torch
+        if stream is None:
+            stream = torch.cuda.current_stream(self.device)
+        s = ctypes.c_void_p(stream.cuda_stream)
+        _lib.check(self._L.mpcqp_fleet_run(self._nominal._ws, self._relaxed._ws, ctypes.byref(self._fleet),
+                                           int(steps), int(self.use_graph), s), "mpcqp_fleet_run")
+
+    def running(self) -> int:
+        return int((self._bufs["phase"][: self.vehicles] == _lib.FLEET_RUNNING).sum().item())
+
+    def run(self, sim_steps: Optional[int] = None, check_every: int = 16) -> FleetResult:
+        """Step until every vehicle has left the RUNNING phase (or ``sim_steps`` steps)."""
+        total = self.max_steps if sim_steps is None else min(int(sim_steps), self.max_steps)
+        done = 0
+        while done < total and self.vehicles:
+            k = min(check_every, total - done)
+            self.step(k)
+            done += k
+            if self.running() == 0:
+                break
+        return self.result()
+
+    def result(self) -> FleetResult:
+        b = self._bufs
+        V = self.vehicles
+        self._torch.cuda.synchronize(self.device)
+        steps = b["steps"][:V].cpu().numpy().copy()
+        trace = b["trace"][:V].cpu().numpy()
+        utr = b["u_trace"][:V].cpu().numpy()
+        return FleetResult(
+            states=[trace[v, : steps[v]].copy() for v in range(V)],
+            inputs=[utr[v, : steps[v]].copy() for v in range(V)],
+            phase=b["phase"][:V].cpu().numpy().copy(),
+            steps=steps,
+            path_idx=b["path_idx"][:V].cpu().numpy().copy(),
+        )
+
+    def buffers(self) -> dict:
+        """The device tensors behind the fleet state (views; for inspection and tests)."""
+        return self._bufs
+
+    def close(self) -> None:
+        self._nominal.close()
+        self._relaxed.close()
+
+
+__all__ = ["FleetTracker", "FleetResult", "relaxed_parameters", "initial_state", "PHASE_NAMES"]

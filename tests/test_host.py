@@ -40,23 +40,45 @@ def test_library_exports_every_header_symbol():
     assert L.mpcqp_model_stride(20) % 8 == 0
 
 
-def test_param_struct_layout_matches_c(tmp_path):
-    """ctypes mirror of mpcqp_params == the C compiler's layout (sizeof and every offset)."""
-    from mpcqp._lib import MpcqpParams
+@pytest.mark.parametrize("cls_name,c_name", [("MpcqpParams", "mpcqp_params"), ("MpcqpFleet", "mpcqp_fleet")])
+def test_struct_layout_matches_c(tmp_path, cls_name, c_name):
+    """ctypes mirrors of mpcqp_params / mpcqp_fleet == the C compiler's layout (sizeof, offsets)."""
+    from mpcqp import _lib
 
-    fields = [f for f, _ in MpcqpParams._fields_]
+    cls = getattr(_lib, cls_name)
+    fields = [f for f, _ in cls._fields_]
     src = tmp_path / "layout.c"
     src.write_text(
         '#include <stdio.h>\n#include <stddef.h>\n#include "mpcqp.h"\nint main(void){\n'
-        '  printf("%zu\\n", sizeof(mpcqp_params));\n'
-        + "".join(f'  printf("%zu\\n", offsetof(mpcqp_params, {f}));\n' for f in fields)
+        f'  printf("%zu\\n", sizeof({c_name}));\n'
+        + "".join(f'  printf("%zu\\n", offsetof({c_name}, {f}));\n' for f in fields)
         + "  return 0;\n}\n")
     exe = tmp_path / "layout"
     subprocess.run(["gcc", "-I", str(ROOT / "include"), "-o", str(exe), str(src)], check=True)
     vals = [int(v) for v in subprocess.run([str(exe)], check=True, capture_output=True, text=True).stdout.split()]
-    assert vals[0] == ctypes.sizeof(MpcqpParams)
+    assert vals[0] == ctypes.sizeof(cls)
     for f, off in zip(fields, vals[1:]):
-        assert getattr(MpcqpParams, f).offset == off, f
+        assert getattr(cls, f).offset == off, f
+
+
+def test_fleet_host_helpers_mirror_control_stage():
+    """relaxed_parameters == the retry parameters of control_stage.py:50-56; initial_state ==
+    :74-79; the fleet phase codes mirror include/mpcqp.h."""
+    from mpcqp import _lib
+    from mpcqp.config import MPCConfig
+    from mpcqp.pipeline.fleet import initial_state, relaxed_parameters
+
+    base = MPCConfig(horizon=10).to_parameters(0.8)
+    rel = relaxed_parameters(base)
+    assert rel.du_bounds == ((-17.0, 17.0), (-0.2, 0.2))
+    assert rel.u_bounds == base.u_bounds and rel.horizon == base.horizon
+    np.testing.assert_array_equal(initial_state([(0.0, 0.0), (1.0, 1.0)], (3.0, 4.0)),
+                                  [3.0, 4.0, np.arctan2(1.0, 1.0), 5.0])
+    np.testing.assert_array_equal(initial_state([(2.0, 2.0)], (3.0, 4.0)), [3.0, 4.0, 0.0, 5.0])
+    text = HEADER.read_text()
+    for name in ("RUNNING", "GOAL", "ABORTED", "OUT_OF_STEPS"):
+        m = re.search(rf"#define MPCQP_FLEET_{name}\s+(\d+)", text)
+        assert m and int(m.group(1)) == getattr(_lib, f"FLEET_{name}")
 
 
 def test_to_c_params_carries_reference_settings():
