@@ -18,15 +18,12 @@ struct SetupSmem {
 };
 
 template <int N>
-__global__ __launch_bounds__(kWave) void k_setup(mpcqp_params p, int B, const uint8_t* __restrict__ mask,
-                                                 const double* __restrict__ model, double* __restrict__ state) {
+__device__ __forceinline__ void setup_qp(const mpcqp_params& p, int b, const double* __restrict__ model,
+                                         double* __restrict__ state, SetupSmem<N>& sm) {
   constexpr int n = 2 * N;
   constexpr int LD = SetupSmem<N>::LD;
   constexpr int S = model_stride(N);
-  __shared__ SetupSmem<N> sm;
-  const int b = blockIdx.x;
   const int lane = threadIdx.x;
-  if (b >= B || (mask && !mask[b])) return;
   const bool act = lane < n;
   const bool even = act && ((lane & 1) == 0);
   const int cc = lane & 1;  // 0 = acceleration, 1 = steering
@@ -465,11 +462,8 @@ struct SolveSmem {
 
 // ------------------------------------------------------------------ K2b: ADMM
 template <int N>
-__global__ __launch_bounds__(kWave) void k_admm(mpcqp_params p, int B, const uint8_t* __restrict__ mask,
-                                                double* __restrict__ state) {
-  __shared__ SolveSmem<N> sm;
-  const int b = blockIdx.x;
-  if (b >= B || (mask && !mask[b])) return;
+__device__ __forceinline__ void admm_qp(const mpcqp_params& p, int b, double* __restrict__ state,
+                                        SolveSmem<N>& sm) {
   double* st = state + (size_t)b * state_stride(N);
   Ctx<N> C;
   C.load(st, threadIdx.x, p.dt, sm.buf, sm.sv, sm.Dl, sm.P);
@@ -610,16 +604,12 @@ __global__ __launch_bounds__(kWave) void k_admm(mpcqp_params p, int B, const uin
 
 // ------------------------------------------------------------------ K2c: polish + outputs
 template <int N>
-__global__ __launch_bounds__(kWave) void k_finish(mpcqp_params p, int B, const uint8_t* __restrict__ mask,
-                                                  const double* __restrict__ model,
-                                                  const double* __restrict__ state, double* __restrict__ u0o,
-                                                  double* __restrict__ Xo, double* __restrict__ Uo,
-                                                  int32_t* __restrict__ statuso, int32_t* __restrict__ iterso,
-                                                  uint8_t* __restrict__ activeo) {
+__device__ __forceinline__ void finish_qp(const mpcqp_params& p, int b, const double* __restrict__ model,
+                                          const double* __restrict__ state, double* __restrict__ u0o,
+                                          double* __restrict__ Xo, double* __restrict__ Uo,
+                                          int32_t* __restrict__ statuso, int32_t* __restrict__ iterso,
+                                          uint8_t* __restrict__ activeo, SolveSmem<N>& sm) {
   constexpr int n = 2 * N;
-  __shared__ SolveSmem<N> sm;
-  const int b = blockIdx.x;
-  if (b >= B || (mask && !mask[b])) return;
   const int lane = threadIdx.x;
   const double* st = state + (size_t)b * state_stride(N);
   Ctx<N> C;
@@ -840,15 +830,41 @@ __global__ __launch_bounds__(kWave) void k_finish(mpcqp_params p, int B, const u
   }
 }
 
+// ------------------------------------------------------------------ K2: fused solve
+// One wave runs its QP through setup -> ADMM -> polish/outputs without kernel boundaries, so
+// the batch drains once (the slowest QP's whole chain) instead of once per phase.  The phases
+// hand over through the per-QP state buffer (written and re-read by the same wave, so it stays
+// in this CU's caches) and share the LDS through a union.
+template <int N>
+union SolveLds {
+  SetupSmem<N> setup;
+  SolveSmem<N> solve;
+};
+
+template <int N>
+__global__ __launch_bounds__(kWave) void k_solve(mpcqp_params p, int B, const uint8_t* __restrict__ mask,
+                                                 const double* __restrict__ model, double* __restrict__ state,
+                                                 double* __restrict__ u0o, double* __restrict__ Xo,
+                                                 double* __restrict__ Uo, int32_t* __restrict__ statuso,
+                                                 int32_t* __restrict__ iterso, uint8_t* __restrict__ activeo) {
+  __shared__ SolveLds<N> sm;
+  const int b = blockIdx.x;
+  if (b >= B || (mask && !mask[b])) return;
+  setup_qp<N>(p, b, model, state, sm.setup);
+  __syncthreads();
+  if (p.method == MPCQP_METHOD_ADMM) {
+    admm_qp<N>(p, b, state, sm.solve);
+    __syncthreads();
+  }
+  finish_qp<N>(p, b, model, state, u0o, Xo, Uo, statuso, iterso, activeo, sm.solve);
+}
+
 }  // namespace
 
 namespace mpcqp {
 template <int N>
 void launch_solve(hipStream_t s, const Launch& L) {
-  hipLaunchKernelGGL(k_setup<N>, dim3(L.B), dim3(kWave), 0, s, *L.p, L.B, L.mask, L.model, L.state);
-  if (L.p->method == MPCQP_METHOD_ADMM)
-    hipLaunchKernelGGL(k_admm<N>, dim3(L.B), dim3(kWave), 0, s, *L.p, L.B, L.mask, L.state);
-  hipLaunchKernelGGL(k_finish<N>, dim3(L.B), dim3(kWave), 0, s, *L.p, L.B, L.mask, L.model, L.state, L.u0, L.X, L.U,
+  hipLaunchKernelGGL(k_solve<N>, dim3(L.B), dim3(kWave), 0, s, *L.p, L.B, L.mask, L.model, L.state, L.u0, L.X, L.U,
                      L.st, L.it, L.ac);
 }
 

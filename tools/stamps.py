@@ -2,8 +2,11 @@
 """Development tool: per-phase cycle attribution from the -DMPCQP_STAMPS diagnostic build.
 
     hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared -DMPCQP_STAMPS -DMPCQP_ONLY_N=20 \
-        -o build/libmpcqp_stamps.so rrt-mpc_amd/csrc/mpcqp.hip
-    MPCQP_LIB=build/libmpcqp_stamps.so python tools/stamps.py
+        -o tools/diag/libmpcqp_stamps.so rrt-mpc_amd/csrc/mpcqp.hip rrt-mpc_amd/csrc/mpcqp_fleet.hip
+    python tools/stamps.py [config] [--worst K]
+
+--worst K: replicate the K-th slowest QP (by ADMM iterations) over the batch, so the per-QP
+averages are that QP's own breakdown (the tail that sets the kernel's latency).
 
 Stamps serialize around each phase, so read the SHARES, never the absolute run time.
 """
@@ -18,7 +21,7 @@ from pathlib import Path
 import numpy as np
 
 ROOT = Path(__file__).resolve().parents[1]
-os.environ.setdefault("MPCQP_LIB", str(ROOT / "build" / "libmpcqp_stamps.so"))
+os.environ.setdefault("MPCQP_LIB", str(ROOT / "tools" / "diag" / "libmpcqp_stamps.so"))
 sys.path.insert(0, str(ROOT / "rrt-mpc_amd"))
 
 NAMES = {0: "admm.form", 1: "admm.sweep", 2: "admm.iteration", 3: "admm.check", 4: "admm.total",
@@ -32,16 +35,31 @@ def main() -> None:
     from mpcqp.config import MPCConfig
     from mpcqp.control.mpc_controller import BatchedMPCController
 
-    cfg = sys.argv[1] if len(sys.argv) > 1 else "config3"
-    b = getattr(scenarios, cfg)()
-    B = b.size
-    ctrl = BatchedMPCController(MPCConfig(horizon=b.horizon).to_parameters(0.8), B, device="cuda:0")
+    import argparse
+
+    ap = argparse.ArgumentParser()
+    ap.add_argument("config", nargs="?", default="config3")
+    ap.add_argument("--worst", type=int, default=-1)
+    ap.add_argument("--batch", type=int, default=0)
+    a = ap.parse_args()
+    b = getattr(scenarios, a.config)()
+    x0, ref, up = b.x0, b.ref, b.u_prev
+    B = a.batch or b.size
+    ctrl = BatchedMPCController(MPCConfig(horizon=b.horizon).to_parameters(0.8), max(B, b.size), device="cuda:0")
     L = _lib.lib()
     buf = (ctypes.c_ulonglong * 16)()
-    ctrl.solve_batch(b.x0, b.ref, b.u_prev)
+    ctrl.solve_batch(x0, ref, up)
+    torch.cuda.synchronize()
+    if a.worst >= 0:
+        order = np.argsort(-ctrl._iters[: b.size, 0].cpu().numpy(), kind="stable")
+        q = int(order[a.worst])
+        x0, ref, up = (np.repeat(v[q:q + 1], B, axis=0) for v in (x0, ref, up))
+    else:
+        x0, ref, up = x0[:B], ref[:B], up[:B]
+    ctrl.solve_batch(x0, ref, up)
     torch.cuda.synchronize()
     _lib.check(L.mpcqp_debug_stamps(buf, 1), "stamps reset")
-    ctrl.solve_batch(b.x0, b.ref, b.u_prev)
+    ctrl.solve_batch(x0, ref, up)
     torch.cuda.synchronize()
     _lib.check(L.mpcqp_debug_stamps(buf, 0), "stamps read")
     it = ctrl._iters[:B].cpu().numpy()
