@@ -94,7 +94,7 @@ typedef struct mpcqp_params {
   int32_t adaptive_rho_interval; /* 25 (deterministic; OSQP's default is timing based) */
   int32_t polish;             /* 1 */
   int32_t polish_max_iter;    /* 100 */
-  int32_t reserved;
+  int32_t debug_state;        /* 1: also write the per-QP solver state buffer (mpcqp_state_buffer; tests) */
 } mpcqp_params;
 
 typedef struct mpcqp_ws mpcqp_ws;
@@ -205,7 +205,7 @@ int mpcqp_debug_wave_ops(const double* in, double* out, void* stream);
 
 /* Diagnostic builds only (-DMPCQP_STAMPS; the measured library returns MPCQP_E_ARG):
  * per-phase s_memtime cycle sums over all waves since the last reset. */
-int mpcqp_debug_stamps(unsigned long long* out16, int reset);
+int mpcqp_debug_stamps(unsigned long long* out32, int reset);
 
 #ifdef __cplusplus
 }

@@ -47,7 +47,7 @@ class CParams(ctypes.Structure):
         ("adaptive_rho_interval", ctypes.c_int32),
         ("polish", ctypes.c_int32),
         ("polish_max_iter", ctypes.c_int32),
-        ("reserved", ctypes.c_int32),
+        ("debug_state", ctypes.c_int32),
     ]
 
 

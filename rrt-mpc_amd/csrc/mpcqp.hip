@@ -193,18 +193,18 @@ const double* mpcqp_state_buffer(const mpcqp_ws* ws) { return ws ? ws->state : n
 
 int mpcqp_state_stride(int horizon) { return state_stride(horizon); }
 
-int mpcqp_debug_stamps(unsigned long long* out16, int reset) {
+int mpcqp_debug_stamps(unsigned long long* out32, int reset) {
 #ifdef MPCQP_STAMPS
   hipError_t e = hipDeviceSynchronize();
-  if (e == hipSuccess && out16) e = hipMemcpyFromSymbol(out16, HIP_SYMBOL(g_stamps), sizeof(unsigned long long) * 16);
+  if (e == hipSuccess && out32) e = hipMemcpyFromSymbol(out32, HIP_SYMBOL(g_stamps), sizeof(unsigned long long) * 32);
   if (e == hipSuccess && reset) {
-    unsigned long long z[16] = {0};
+    unsigned long long z[32] = {0};
     e = hipMemcpyToSymbol(HIP_SYMBOL(g_stamps), z, sizeof(z));
   }
   if (e != hipSuccess) return fail(MPCQP_E_HIP, std::string("stamps: ") + hipGetErrorString(e));
   return MPCQP_OK;
 #else
-  (void)out16;
+  (void)out32;
   (void)reset;
   return fail(MPCQP_E_ARG, "not a -DMPCQP_STAMPS diagnostic build");
 #endif

@@ -70,18 +70,26 @@ constexpr int kRowShr1 = 0x111, kRowShr2 = 0x112, kRowShr4 = 0x114, kRowShr8 = 0
 constexpr int kRowShl1 = 0x101, kRowShl2 = 0x102, kRowShl4 = 0x104, kRowShl8 = 0x108;
 constexpr int kWaveShr1 = 0x138, kWaveShl1 = 0x130;
 
-// inclusive prefix sum over lanes 0..lane (zero-filled row shifts + row totals)
+// DPP with a row mask: rows outside ROWMASK read 0
+template <int CTRL, int ROWMASK>
+__device__ __forceinline__ double dpp_rows(double v) {
+  const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), CTRL, ROWMASK, 0xf, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), CTRL, ROWMASK, 0xf, false);
+  return __hiloint2double(hi, lo);
+}
+constexpr int kRowBcast15 = 0x142, kRowBcast31 = 0x143;  // GFX9 wave-level row broadcasts
+
+// inclusive prefix sum over lanes 0..lane: zero-filled row shifts, then the row totals carried
+// across rows by row_bcast:15 (rows 1, 3) and row_bcast:31 (rows 2, 3) -- no SGPR round trip
 __device__ __forceinline__ double scan_add(double v, int lane) {
+  (void)lane;
   v += dpp<kRowShr1>(v);
   v += dpp<kRowShr2>(v);
   v += dpp<kRowShr4>(v);
   v += dpp<kRowShr8>(v);
-  const double t0 = readlane(v, 15), t1 = readlane(v, 31), t2 = readlane(v, 47);
-  const int row = lane >> 4;
-  double off = row >= 1 ? t0 : 0.0;
-  if (row >= 2) off += t1;
-  if (row >= 3) off += t2;
-  return v + off;
+  v += dpp_rows<kRowBcast15, 0xa>(v);
+  v += dpp_rows<kRowBcast31, 0xc>(v);
+  return v;
 }
 // inclusive suffix sum over lanes lane..63
 __device__ __forceinline__ double rscan_add(double v, int lane) {
@@ -121,20 +129,16 @@ __device__ __forceinline__ double rscan_max(double v, int lane) {
   if (row <= 0) off = fmax(off, t1);
   return fmax(v, off);
 }
-// wave-uniform sum / max (row scans + four row totals)
-__device__ __forceinline__ double wave_sum(double v) {
-  v += dpp<kRowShr1>(v);
-  v += dpp<kRowShr2>(v);
-  v += dpp<kRowShr4>(v);
-  v += dpp<kRowShr8>(v);
-  return (readlane(v, 15) + readlane(v, 31)) + (readlane(v, 47) + readlane(v, 63));
-}
+// wave-uniform sum / max: the inclusive scan's last lane
+__device__ __forceinline__ double wave_sum(double v) { return readlane(scan_add(v, 0), 63); }
 __device__ __forceinline__ double wave_max(double v) {  // v >= 0
   v = fmax(v, dpp<kRowShr1>(v));
   v = fmax(v, dpp<kRowShr2>(v));
   v = fmax(v, dpp<kRowShr4>(v));
   v = fmax(v, dpp<kRowShr8>(v));
-  return fmax(fmax(readlane(v, 15), readlane(v, 31)), fmax(readlane(v, 47), readlane(v, 63)));
+  v = fmax(v, dpp_rows<kRowBcast15, 0xa>(v));
+  v = fmax(v, dpp_rows<kRowBcast31, 0xc>(v));
+  return readlane(v, 63);
 }
 // lane i <- lane i-2 (0 for i < 2);  lane i <- lane i+2 (0 past the wave)
 __device__ __forceinline__ double shr2(double v) { return dpp<kWaveShr1>(dpp<kWaveShr1>(v)); }
@@ -194,7 +198,7 @@ __device__ __forceinline__ void lds_sync() { __builtin_amdgcn_fence(__ATOMIC_SEQ
 // Built only with -DMPCQP_STAMPS (never in the measured library): per-phase s_memtime
 // cycle sums, flushed once per wave into g_stamps[] (read by mpcqp_debug_stamps).
 #ifdef MPCQP_STAMPS
-__device__ unsigned long long g_stamps[16];
+__device__ unsigned long long g_stamps[32];
 struct Stamps {
   unsigned long long acc[6] = {0, 0, 0, 0, 0, 0};
   unsigned long long t = 0;

@@ -1,4 +1,4 @@
-// mpcqp_solve.h -- K2a/K2b/K2c solver kernels, templated on the horizon N.
+// mpcqp_solve.h -- K2 solver kernel (setup -> ADMM -> polish), templated on the horizon N.
 #pragma once
 #include "mpcqp_common.h"
 
@@ -8,8 +8,6 @@ using mpcqp::Launch;
 template <int N>
 struct SetupSmem {
   static constexpr int n = 2 * N;
-  static constexpr int LD = n + 1;  // odd: conflict-free row and column access
-  double P[n * LD];
   double buf[kWave];
   double model[model_stride(N)];
   double pre[4][N + 1];  // prefix sums of alpha, beta, gamma, eta
@@ -18,250 +16,16 @@ struct SetupSmem {
 };
 
 template <int N>
-__device__ __forceinline__ void setup_qp(const mpcqp_params& p, int b, const double* __restrict__ model,
-                                         double* __restrict__ state, SetupSmem<N>& sm) {
-  constexpr int n = 2 * N;
-  constexpr int LD = SetupSmem<N>::LD;
-  constexpr int S = model_stride(N);
-  const int lane = threadIdx.x;
-  const bool act = lane < n;
-  const bool even = act && ((lane & 1) == 0);
-  const int cc = lane & 1;  // 0 = acceleration, 1 = steering
-  const double dt = p.dt;
+struct SolveSmem {
+  double P[4 * N * N];  // Pbar, row-major n x n (lane `col` reads column col: conflict-free)
+  double sv[N + 1];     // suffix sums of the v-row weights (form)
+};
 
-  {
-    const double* mb = model + (size_t)b * S;
-    for (int i = lane; i < S; i += kWave) sm.model[i] = mb[i];
-  }
-  __syncthreads();
-  const double* al = sm.model;
-  const double* be = sm.model + N;
-  const double* ga = sm.model + 2 * N;
-  const double* et = sm.model + 3 * N;
-  const double* si = sm.model + 4 * N;
-  const double* c0 = sm.model + 5 * N;
-  const double* c1 = sm.model + 6 * N;
-  const double* rr = sm.model + 7 * N;
-  const double* x0 = sm.model + 11 * N + 4;
-  const double* up = sm.model + 11 * N + 8;
-
-  // prefix sums (lanes 0..3, one array each) and free response (lane 4)
-  if (lane < 4) {
-    const double* a = sm.model + lane * N;
-    double acc = 0.0;
-    sm.pre[lane][0] = 0.0;
-    for (int k = 0; k < N; ++k) {
-      acc += a[k];
-      sm.pre[lane][k + 1] = acc;
-    }
-  } else if (lane == 4) {
-    double px = x0[0], py = x0[1];
-    const double psi = x0[2], v = x0[3];
-    for (int m = 1; m <= N; ++m) {
-      const int k = m - 1;
-      px = px + al[k] * psi + be[k] * v + c0[k];
-      py = py + ga[k] * psi + et[k] * v + c1[k];
-      sm.err[m][0] = px - rr[4 * m + 0];
-      sm.err[m][1] = py - rr[4 * m + 1];
-      sm.err[m][2] = psi - rr[4 * m + 2];
-      sm.err[m][3] = v - rr[4 * m + 3];
-    }
-  }
-  __syncthreads();
-
-  // ---- condense: column `lane` of H (lane n -> g) by the backward adjoint recursion ----
-  // mu_m = W_m s_m + A_m' mu_{m+1};  H[(i,c'), col] = (B_i e_c')' mu_{i+1}
-  if (lane <= n) {
-    double Q[4][4], QN[4][4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        Q[i][j] = 0.5 * (p.q[4 * i + j] + p.q[4 * j + i]);
-        QN[i][j] = 0.5 * (p.q_terminal[4 * i + j] + p.q_terminal[4 * j + i]);
-      }
-    const int j = lane >> 1;
-    const bool gcol = lane == n;
-    const double sj = gcol ? 0.0 : si[j];
-    const double pa0 = gcol ? 0.0 : sm.pre[0][j + 1], pb0 = gcol ? 0.0 : sm.pre[1][j + 1];
-    const double pg0 = gcol ? 0.0 : sm.pre[2][j + 1], pe0 = gcol ? 0.0 : sm.pre[3][j + 1];
-    double mu0 = 0.0, mu1 = 0.0, mu2 = 0.0, mu3 = 0.0;
-    for (int m = N; m >= 1; --m) {
-      double s0, s1, s2, s3;
-      if (gcol) {
-        s0 = sm.err[m][0];
-        s1 = sm.err[m][1];
-        s2 = sm.err[m][2];
-        s3 = sm.err[m][3];
-      } else if (m > j) {
-        if (cc == 0) {
-          s0 = dt * (sm.pre[1][m] - pb0);
-          s1 = dt * (sm.pre[3][m] - pe0);
-          s2 = 0.0;
-          s3 = dt;
-        } else {
-          s0 = sj * (sm.pre[0][m] - pa0);
-          s1 = sj * (sm.pre[2][m] - pg0);
-          s2 = sj;
-          s3 = 0.0;
-        }
-      } else {
-        s0 = s1 = s2 = s3 = 0.0;
-      }
-      const bool term = m == N;
-      auto W = [&](int i, int k) -> double { return term ? QN[i][k] : Q[i][k]; };
-      const double w0 = W(0, 0) * s0 + W(0, 1) * s1 + W(0, 2) * s2 + W(0, 3) * s3;
-      const double w1 = W(1, 0) * s0 + W(1, 1) * s1 + W(1, 2) * s2 + W(1, 3) * s3;
-      const double w2 = W(2, 0) * s0 + W(2, 1) * s1 + W(2, 2) * s2 + W(2, 3) * s3;
-      const double w3 = W(3, 0) * s0 + W(3, 1) * s1 + W(3, 2) * s2 + W(3, 3) * s3;
-      if (m < N) {
-        const double m0 = mu0, m1 = mu1;
-        mu0 = w0 + m0;
-        mu1 = w1 + m1;
-        mu2 = w2 + (mu2 + al[m] * m0 + ga[m] * m1);
-        mu3 = w3 + (mu3 + be[m] * m0 + et[m] * m1);
-      } else {
-        mu0 = w0;
-        mu1 = w1;
-        mu2 = w2;
-        mu3 = w3;
-      }
-      const double ha = dt * mu3, hd = si[m - 1] * mu2;
-      if (gcol) {
-        sm.g[2 * (m - 1)] = ha;
-        sm.g[2 * (m - 1) + 1] = hd;
-      } else {
-        sm.P[(2 * (m - 1)) * LD + lane] = ha;
-        sm.P[(2 * (m - 1) + 1) * LD + lane] = hd;
-      }
-    }
-    if (!gcol) {
-      const double R0 = 0.5 * (p.r[0 * 2 + cc] + p.r[cc * 2 + 0]);
-      const double R1 = 0.5 * (p.r[1 * 2 + cc] + p.r[cc * 2 + 1]);
-      sm.P[(2 * j) * LD + lane] += R0;
-      sm.P[(2 * j + 1) * LD + lane] += R1;
-    }
-  }
-  __syncthreads();
-
-  // ---- unscaled data: P = 2H (column `lane`), q = 2g, folded row bounds ----
-  double qv = act ? 2.0 * sm.g[lane] : 0.0;
-  double cmax = 0.0;  // running column max of |P|
-  if (act) {
-#pragma unroll 8
-    for (int i = 0; i < n; ++i) {
-      const double t = 2.0 * sm.P[i * LD + lane];
-      sm.P[i * LD + lane] = t;
-      cmax = fmax(cmax, fabs(t));
-    }
-  }
-  double lo[3], hi[3], wt[3], E[3];
-  {
-    const double off = lane < 2 ? up[cc] : 0.0;
-    lo[0] = even ? p.v_bounds[0] - x0[3] : 0.0;
-    hi[0] = even ? p.v_bounds[1] - x0[3] : 0.0;
-    wt[0] = even ? p.slack_velocity : 0.0;
-    lo[1] = act ? p.u_bounds[2 * cc] : 0.0;
-    hi[1] = act ? p.u_bounds[2 * cc + 1] : 0.0;
-    wt[1] = act ? p.slack_input : 0.0;
-    lo[2] = act ? p.du_bounds[2 * cc] + off : 0.0;
-    hi[2] = act ? p.du_bounds[2 * cc + 1] + off : 0.0;
-    wt[2] = act ? p.slack_rate : 0.0;
-    E[0] = even ? 1.0 : 0.0;
-    E[1] = act ? 1.0 : 0.0;
-    E[2] = act ? 1.0 : 0.0;
-  }
-  double D = act ? 1.0 : 0.0;
-  double cscale = 1.0;
-
-  // ---- Ruiz equilibration + cost scaling (OSQP scale_data, `scaling` iterations) ----
-  for (int it = 0; it < p.scaling; ++it) {
-    // column norms of [P; A] (first n columns of the KKT matrix)
-    const double sufE = rscan_max(E[0], lane);  // max E over v rows >= p/2 (odd lanes carry 0)
-    const double e2n = shl2(E[2]);
-    double ccol = fmax(E[1], E[2]);
-    if (lane + 2 < n) ccol = fmax(ccol, e2n);
-    if (even) ccol = fmax(ccol, dt * sufE);
-    ccol *= D;
-    const double dl = act ? 1.0 / sqrt(limit_scaling(fmax(cmax, ccol))) : 0.0;
-    // row norms of A
-    const double preD = scan_max(even ? D : 0.0, lane);
-    const double Dm2 = shr2(D);
-    const double el0 = even ? 1.0 / sqrt(limit_scaling(E[0] * dt * preD)) : 0.0;
-    const double el1 = act ? 1.0 / sqrt(limit_scaling(E[1] * D)) : 0.0;
-    const double el2 = act ? 1.0 / sqrt(limit_scaling(E[2] * (lane >= 2 ? fmax(D, Dm2) : D))) : 0.0;
-    // apply: P <- dl P dl (column `lane`), q <- dl q
-    __syncthreads();
-    sm.buf[lane] = dl;
-    __syncthreads();
-    double cm2 = 0.0;
-    if (act) {
-#pragma unroll 8
-      for (int i = 0; i < n; ++i) {
-        const double t = sm.P[i * LD + lane] * (sm.buf[i] * dl);
-        sm.P[i * LD + lane] = t;
-        cm2 = fmax(cm2, fabs(t));
-      }
-    }
-    D *= dl;
-    qv *= dl;
-    E[0] *= el0;
-    E[1] *= el1;
-    E[2] *= el2;
-    // cost scaling
-    const double cn = wave_sum(act ? cm2 : 0.0) / n;
-    const double qn = limit_scaling(wave_max(fabs(qv)));
-    const double ct = 1.0 / limit_scaling(fmax(cn, qn));
-    if (act) {
-#pragma unroll 8
-      for (int i = 0; i < n; ++i) sm.P[i * LD + lane] *= ct;
-    }
-    qv *= ct;
-    cmax = cm2 * ct;
-    cscale *= ct;
-  }
-  __syncthreads();
-
-  // ---- write the solver state ----
-  double* st = state + (size_t)b * state_stride(N);
-  bool finite = isfinite(qv) && isfinite(cscale);
-  if (act) {
-    // symmetric Pbar: the lower-triangle value (computed by column `min`) for both halves
-    for (int i = 0; i < n; ++i) {
-      const double v = i >= lane ? sm.P[i * LD + lane] : sm.P[lane * LD + i];
-      finite = finite && isfinite(v);
-      st[i * n + lane] = v;
-    }
-  }
-  double* lf = st + state_lane_off(N);
-  double wb[3];
-#pragma unroll
-  for (int r = 0; r < 3; ++r) {
-    lo[r] *= E[r];
-    hi[r] *= E[r];
-    wb[r] = E[r] > 0.0 ? cscale * wt[r] / (E[r] * E[r]) : 0.0;
-    finite = finite && isfinite(lo[r]) && isfinite(hi[r]);
-  }
-  // non-finite data (NaN/inf in x0, ref or u_prev) -> status MPCQP_NUMERICAL_ERROR
-  const bool bad_input = wave_any(!finite);
-  lf[kFq * kWave + lane] = qv;
-  lf[kFD * kWave + lane] = D;
-  lf[kFx * kWave + lane] = 0.0;
-#pragma unroll
-  for (int r = 0; r < 3; ++r) {
-    lf[(kFE0 + r) * kWave + lane] = E[r];
-    lf[(kFlo0 + r) * kWave + lane] = lo[r];
-    lf[(kFhi0 + r) * kWave + lane] = hi[r];
-    lf[(kFw0 + r) * kWave + lane] = wb[r];
-  }
-  if (lane == 0) {
-    double* sc = st + state_scal_off(N);
-    sc[0] = cscale;
-    sc[1] = bad_input ? -1.0 : 0.0;  // ADMM flag: -1 numerical error, 0 not converged, 1 converged
-    sc[2] = 0.0;                     // admm iterations
-    sc[3] = 0.0;                     // factorizations
-  }
-}
+template <int N>
+union SolveLds {
+  SetupSmem<N> setup;
+  SolveSmem<N> solve;  // setup_qp writes Pbar when its own LDS data is dead
+};
 
 // ------------------------------------------------------------------ shared solver context
 // Per-lane view of one scaled QP plus the structured operators and the KKT inverse.
@@ -274,39 +38,21 @@ struct Ctx {
   double D, qv;
   double E[3], lo[3], hi[3], wb[3];
   double cscale;
-  const double* __restrict__ P;  // Pbar (global, L2-resident)
-  double* buf;                   // LDS broadcast buffer, >= 2*kWave doubles
+  const double* __restrict__ P;  // Pbar (LDS, row-major n x n)
   double* sv;                    // LDS, N+1 doubles
-  double* Dl;                    // LDS copy of D (n doubles)
   static constexpr int kNW = (n + 15) / 16;  // 16-lane rows holding the n variables
   // KKT inverse, row `lane`: A^{-1}[lane][j] = -r[j] (symmetric sweep operator)
   double r[n];
 
-  __device__ __forceinline__ void load(const double* st, int ln, double dt_, double* buf_, double* sv_, double* Dl_,
-                                       double* Ps) {
+  // Bind the context to this lane and the solve LDS (Pbar, broadcast buffers); the problem
+  // data fields are filled by setup_qp.
+  __device__ __forceinline__ void init(int ln, double dt_, SolveSmem<N>& s) {
     lane = ln;
     act = ln < n;
     even = act && ((ln & 1) == 0);
     dt = dt_;
-    buf = buf_;
-    sv = sv_;
-    Dl = Dl_;
-    // Pbar is re-read by every factorization and every P-product: stage it in LDS once
-    for (int i = ln; i < n * n; i += kWave) Ps[i] = st[i];
-    P = Ps;
-    const double* lf = st + state_lane_off(N);
-    qv = lf[kFq * kWave + ln];
-    D = lf[kFD * kWave + ln];
-#pragma unroll
-    for (int k = 0; k < 3; ++k) {
-      E[k] = lf[(kFE0 + k) * kWave + ln];
-      lo[k] = lf[(kFlo0 + k) * kWave + ln];
-      hi[k] = lf[(kFhi0 + k) * kWave + ln];
-      wb[k] = lf[(kFw0 + k) * kWave + ln];
-    }
-    cscale = st[state_scal_off(N)];
-    if (act) Dl[ln] = D;
-    __syncthreads();
+    sv = s.sv;
+    P = s.P;
   }
 
   // Make the per-lane problem data opaque to the optimizer at the top of a solver
@@ -452,26 +198,313 @@ struct Ctx {
   }
 };
 
+// ------------------------------------------------------------------ K2 phase 1: setup
+// Condensing (states and slacks eliminated) + OSQP Ruiz/cost scaling.  Leaves the scaled
+// problem on chip for the later phases: Pbar (symmetric, row-major) in the solve LDS, the
+// per-lane data in C.  Returns true on non-finite problem data.  dbg (debug_state builds of
+// the parameter block only) receives the solver state for inspection.
+// Row slots owned by lane p (p < n = 2N):
+//   slot 0: v row (p even): v_{p/2+1} - v0 = dt * sum_{j<=p/2} a_j   (mpc_controller.py:81-82,115-116)
+//   slot 1: input row        U_p                                      (:83-86)
+//   slot 2: rate row         U_p - U_{p-2} (u_prev at k = 0)          (:89-106)
 template <int N>
-struct SolveSmem {
-  double P[4 * N * N];  // Pbar, row-major n x n (column reads by lane are conflict-free)
-  double buf[2 * kWave];
-  double sv[N + 1];
-  double Dl[2 * N];
-};
+__device__ __forceinline__ bool setup_qp(const mpcqp_params& p, int b, const double* __restrict__ model, Ctx<N>& C,
+                                         SolveLds<N>& lds, double* __restrict__ scratch, double* __restrict__ dbg) {
+  constexpr int n = 2 * N;
+  SetupSmem<N>& sm = lds.setup;
+  (void)scratch;
+  constexpr int S = model_stride(N);
+  const int lane = threadIdx.x;
+  const bool act = lane < n;
+  const bool even = act && ((lane & 1) == 0);
+  const int cc = lane & 1;  // 0 = acceleration, 1 = steering
+  const double dt = p.dt;
+  Stamps T, T2;
+  T2.begin();
+  T.begin();
+
+  {
+    const double* mb = model + (size_t)b * S;
+    for (int i = lane; i < S; i += kWave) sm.model[i] = mb[i];
+  }
+  __syncthreads();
+  const double* al = sm.model;
+  const double* be = sm.model + N;
+  const double* ga = sm.model + 2 * N;
+  const double* et = sm.model + 3 * N;
+  const double* si = sm.model + 4 * N;
+  const double* c0 = sm.model + 5 * N;
+  const double* c1 = sm.model + 6 * N;
+  const double* rr = sm.model + 7 * N;
+  const double* x0 = sm.model + 11 * N + 4;
+  const double* up = sm.model + 11 * N + 8;
+
+  // prefix sums (lanes 0..3, one array each) and free response (lane 4)
+  if (lane < 4) {
+    const double* a = sm.model + lane * N;
+    double acc = 0.0;
+    sm.pre[lane][0] = 0.0;
+    for (int k = 0; k < N; ++k) {
+      acc += a[k];
+      sm.pre[lane][k + 1] = acc;
+    }
+  } else if (lane == 4) {
+    double px = x0[0], py = x0[1];
+    const double psi = x0[2], v = x0[3];
+    for (int m = 1; m <= N; ++m) {
+      const int k = m - 1;
+      px = px + al[k] * psi + be[k] * v + c0[k];
+      py = py + ga[k] * psi + et[k] * v + c1[k];
+      sm.err[m][0] = px - rr[4 * m + 0];
+      sm.err[m][1] = py - rr[4 * m + 1];
+      sm.err[m][2] = psi - rr[4 * m + 2];
+      sm.err[m][3] = v - rr[4 * m + 3];
+    }
+  }
+  __syncthreads();
+  T.end(0);
+  T.begin();
+
+  // ---- condense: column `lane` of H (lane n -> g) by the backward adjoint recursion ----
+  // mu_m = W_m s_m + A_m' mu_{m+1};  H[(i,c'), col] = (B_i e_c')' mu_{i+1}
+  // The column stays in registers (Pc) through the scaling; static indices need the m loop
+  // fully unrolled.
+  double Pc[n];
+#pragma unroll
+  for (int i = 0; i < n; ++i) Pc[i] = 0.0;
+  if (lane <= n) {
+    double Q[4][4], QN[4][4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        Q[i][j] = 0.5 * (p.q[4 * i + j] + p.q[4 * j + i]);
+        QN[i][j] = 0.5 * (p.q_terminal[4 * i + j] + p.q_terminal[4 * j + i]);
+      }
+    const int j = lane >> 1;
+    const bool gcol = lane == n;
+    const double sj = gcol ? 0.0 : si[j];
+    const double pa0 = gcol ? 0.0 : sm.pre[0][j + 1], pb0 = gcol ? 0.0 : sm.pre[1][j + 1];
+    const double pg0 = gcol ? 0.0 : sm.pre[2][j + 1], pe0 = gcol ? 0.0 : sm.pre[3][j + 1];
+    double mu0 = 0.0, mu1 = 0.0, mu2 = 0.0, mu3 = 0.0;
+#pragma unroll
+    for (int m = N; m >= 1; --m) {
+      double s0, s1, s2, s3;
+      if (gcol) {
+        s0 = sm.err[m][0];
+        s1 = sm.err[m][1];
+        s2 = sm.err[m][2];
+        s3 = sm.err[m][3];
+      } else if (m > j) {
+        if (cc == 0) {
+          s0 = dt * (sm.pre[1][m] - pb0);
+          s1 = dt * (sm.pre[3][m] - pe0);
+          s2 = 0.0;
+          s3 = dt;
+        } else {
+          s0 = sj * (sm.pre[0][m] - pa0);
+          s1 = sj * (sm.pre[2][m] - pg0);
+          s2 = sj;
+          s3 = 0.0;
+        }
+      } else {
+        s0 = s1 = s2 = s3 = 0.0;
+      }
+      const bool term = m == N;
+      auto W = [&](int i, int k) -> double { return term ? QN[i][k] : Q[i][k]; };
+      const double w0 = W(0, 0) * s0 + W(0, 1) * s1 + W(0, 2) * s2 + W(0, 3) * s3;
+      const double w1 = W(1, 0) * s0 + W(1, 1) * s1 + W(1, 2) * s2 + W(1, 3) * s3;
+      const double w2 = W(2, 0) * s0 + W(2, 1) * s1 + W(2, 2) * s2 + W(2, 3) * s3;
+      const double w3 = W(3, 0) * s0 + W(3, 1) * s1 + W(3, 2) * s2 + W(3, 3) * s3;
+      if (m < N) {
+        const double m0 = mu0, m1 = mu1;
+        mu0 = w0 + m0;
+        mu1 = w1 + m1;
+        mu2 = w2 + (mu2 + al[m] * m0 + ga[m] * m1);
+        mu3 = w3 + (mu3 + be[m] * m0 + et[m] * m1);
+      } else {
+        mu0 = w0;
+        mu1 = w1;
+        mu2 = w2;
+        mu3 = w3;
+      }
+      const double ha = dt * mu3, hd = si[m - 1] * mu2;
+      if (gcol) {
+        sm.g[2 * (m - 1)] = ha;
+        sm.g[2 * (m - 1) + 1] = hd;
+      } else {
+        Pc[2 * (m - 1)] = ha;
+        Pc[2 * (m - 1) + 1] = hd;
+      }
+    }
+    if (!gcol) {
+      const double R0 = 0.5 * (p.r[0 * 2 + cc] + p.r[cc * 2 + 0]);
+      const double R1 = 0.5 * (p.r[1 * 2 + cc] + p.r[cc * 2 + 1]);
+#pragma unroll
+      for (int i = 0; i < n; i += 2)
+        if (i == 2 * j) {
+          Pc[i] += R0;
+          Pc[i + 1] += R1;
+        }
+    }
+  }
+  __syncthreads();
+  if (!act)
+#pragma unroll
+    for (int i = 0; i < n; ++i) Pc[i] = 0.0;  // lane n carried g
+  T.end(1);
+  T.begin();
+
+  // ---- unscaled data: P = 2H (column `lane`), q = 2g, folded row bounds ----
+  double qv = act ? 2.0 * sm.g[lane] : 0.0;
+  double cmax = 0.0;  // running column max of |P|
+#pragma unroll
+  for (int i = 0; i < n; ++i) {
+    Pc[i] = 2.0 * Pc[i];
+    cmax = fmax(cmax, fabs(Pc[i]));
+  }
+  double lo[3], hi[3], wt[3], E[3];
+  {
+    const double off = lane < 2 ? up[cc] : 0.0;
+    lo[0] = even ? p.v_bounds[0] - x0[3] : 0.0;
+    hi[0] = even ? p.v_bounds[1] - x0[3] : 0.0;
+    wt[0] = even ? p.slack_velocity : 0.0;
+    lo[1] = act ? p.u_bounds[2 * cc] : 0.0;
+    hi[1] = act ? p.u_bounds[2 * cc + 1] : 0.0;
+    wt[1] = act ? p.slack_input : 0.0;
+    lo[2] = act ? p.du_bounds[2 * cc] + off : 0.0;
+    hi[2] = act ? p.du_bounds[2 * cc + 1] + off : 0.0;
+    wt[2] = act ? p.slack_rate : 0.0;
+    E[0] = even ? 1.0 : 0.0;
+    E[1] = act ? 1.0 : 0.0;
+    E[2] = act ? 1.0 : 0.0;
+  }
+  double D = act ? 1.0 : 0.0;
+  double cscale = 1.0;
+  T.end(2);
+  T.begin();
+
+  // ---- Ruiz equilibration + cost scaling (OSQP scale_data, `scaling` iterations) ----
+  for (int it = 0; it < p.scaling; ++it) {
+    // column norms of [P; A] (first n columns of the KKT matrix)
+    const double sufE = rscan_max(E[0], lane);  // max E over v rows >= p/2 (odd lanes carry 0)
+    const double e2n = shl2(E[2]);
+    double ccol = fmax(E[1], E[2]);
+    if (lane + 2 < n) ccol = fmax(ccol, e2n);
+    if (even) ccol = fmax(ccol, dt * sufE);
+    ccol *= D;
+    const double dl = act ? 1.0 / sqrt(limit_scaling(fmax(cmax, ccol))) : 0.0;
+    // row norms of A
+    const double preD = scan_max(even ? D : 0.0, lane);
+    const double Dm2 = shr2(D);
+    const double el0 = even ? 1.0 / sqrt(limit_scaling(E[0] * dt * preD)) : 0.0;
+    const double el1 = act ? 1.0 / sqrt(limit_scaling(E[1] * D)) : 0.0;
+    const double el2 = act ? 1.0 / sqrt(limit_scaling(E[2] * (lane >= 2 ? fmax(D, Dm2) : D))) : 0.0;
+    // apply: P <- dl P dl (column `lane`, the row factors read back from LDS), q <- dl q
+    lds_sync();
+    sm.buf[lane] = dl;
+    lds_sync();
+    double cm2 = 0.0;
+#pragma unroll
+    for (int i = 0; i < n; ++i) {
+      const double t = Pc[i] * (sm.buf[i] * dl);
+      Pc[i] = t;
+      cm2 = fmax(cm2, fabs(t));
+    }
+    D *= dl;
+    qv *= dl;
+    E[0] *= el0;
+    E[1] *= el1;
+    E[2] *= el2;
+    // cost scaling
+    const double cn = wave_sum(act ? cm2 : 0.0) / n;
+    const double qn = limit_scaling(wave_max(fabs(qv)));
+    const double ct = 1.0 / limit_scaling(fmax(cn, qn));
+#pragma unroll
+    for (int i = 0; i < n; ++i) Pc[i] *= ct;
+    qv *= ct;
+    cmax = cm2 * ct;
+    cscale *= ct;
+  }
+  __syncthreads();
+  T.end(3);
+  T.begin();
+
+  // ---- Pbar: symmetric (the lower-triangle value, computed by column min, for both halves),
+  //      moved from the column-per-lane setup layout to the row-major solve layout ----
+  // symmetric Pbar = the lower triangle (row i >= column lane, computed by column `lane`)
+  bool finite = isfinite(qv) && isfinite(cscale);
+  lds_sync();  // setup's LDS data is dead: Pbar overwrites it
+  if (act) {
+    double* Pb = lds.solve.P;
+#pragma unroll
+    for (int i = 0; i < n; ++i)
+      if (i >= lane) {  // entry (i, lane) and its mirror (lane, i)
+        Pb[i * n + lane] = Pc[i];
+        Pb[lane * n + i] = Pc[i];
+        finite = finite && isfinite(Pc[i]);
+      }
+  }
+  double wb[3];
+#pragma unroll
+  for (int r = 0; r < 3; ++r) {
+    lo[r] *= E[r];
+    hi[r] *= E[r];
+    wb[r] = E[r] > 0.0 ? cscale * wt[r] / (E[r] * E[r]) : 0.0;
+    finite = finite && isfinite(lo[r]) && isfinite(hi[r]);
+  }
+  // non-finite data (NaN/inf in x0, ref or u_prev) -> status MPCQP_NUMERICAL_ERROR
+  const bool bad_input = wave_any(!finite);
+  C.init(lane, dt, lds.solve);
+  C.qv = qv;
+  C.D = D;
+  C.cscale = cscale;
+#pragma unroll
+  for (int r = 0; r < 3; ++r) {
+    C.E[r] = E[r];
+    C.lo[r] = lo[r];
+    C.hi[r] = hi[r];
+    C.wb[r] = wb[r];
+  }
+  __syncthreads();
+  if (dbg) {
+    if (act)
+      for (int i = 0; i < n; ++i) dbg[i * n + lane] = lds.solve.P[i * n + lane];
+    double* lf = dbg + state_lane_off(N);
+    lf[kFq * kWave + lane] = qv;
+    lf[kFD * kWave + lane] = D;
+    lf[kFx * kWave + lane] = 0.0;
+#pragma unroll
+    for (int r = 0; r < 3; ++r) {
+      lf[(kFE0 + r) * kWave + lane] = E[r];
+      lf[(kFlo0 + r) * kWave + lane] = lo[r];
+      lf[(kFhi0 + r) * kWave + lane] = hi[r];
+      lf[(kFw0 + r) * kWave + lane] = wb[r];
+    }
+    if (lane == 0) {
+      double* sc = dbg + state_scal_off(N);
+      sc[0] = cscale;
+      sc[1] = bad_input ? -1.0 : 0.0;  // ADMM flag: -1 numerical error, 0 not converged, 1 converged
+      sc[2] = 0.0;                     // admm iterations
+      sc[3] = 0.0;                     // factorizations
+    }
+  }
+  T.end(4);
+  T2.end(0);
+  T.flush(16);   // g_stamps[16..20]: model/prefixes, condensing, unscaled data, Ruiz, Pbar + context
+  T2.flush(21);  // g_stamps[21]: whole setup
+  return bad_input;
+}
 
 // ------------------------------------------------------------------ K2b: ADMM
+// Returns the ADMM flag (-1 numerical error, 0 not converged, 1 converged); x, it, nfact out.
 template <int N>
-__device__ __forceinline__ void admm_qp(const mpcqp_params& p, int b, double* __restrict__ state,
-                                        SolveSmem<N>& sm) {
-  double* st = state + (size_t)b * state_stride(N);
-  Ctx<N> C;
-  C.load(st, threadIdx.x, p.dt, sm.buf, sm.sv, sm.Dl, sm.P);
+__device__ __forceinline__ int admm_qp(const mpcqp_params& p, Ctx<N>& C, bool bad, double& x_out, int& it_out,
+                                       int& nfact_out, double* __restrict__ dbg) {
   const bool act = C.act;
   double x = 0.0, z[3] = {0.0, 0.0, 0.0}, y[3] = {0.0, 0.0, 0.0};
   double rho = p.rho;
   const double sg = p.sigma, alpha = p.alpha;
-  bool bad = st[state_scal_off(N) + 1] < 0.0;  // non-finite problem data (k_setup)
   bool ok = false;
   int it = 0, nfact = 0;
   Stamps T, T2;
@@ -515,11 +548,10 @@ __device__ __forceinline__ void admm_qp(const mpcqp_params& p, int b, double* __
       for (int r = 0; r < 3; ++r) {
         const double v = alpha * zt[r] + (1.0 - alpha) * z[r];
         const double vv = v + y[r] * ir;
-        double zn = vv;
-        if (vv > C.hi[r])
-          zn = prox_a[r] * vv + prox_b[r] * C.hi[r];
-        else if (vv < C.lo[r])
-          zn = prox_a[r] * vv + prox_b[r] * C.lo[r];
+        // branch-free: both clamped candidates, then selects
+        const double zhi = prox_a[r] * vv + prox_b[r] * C.hi[r];
+        const double zlo = prox_a[r] * vv + prox_b[r] * C.lo[r];
+        const double zn = vv > C.hi[r] ? zhi : (vv < C.lo[r] ? zlo : vv);
         y[r] = y[r] + rho * (v - zn);
         z[r] = zn;
       }
@@ -589,41 +621,39 @@ __device__ __forceinline__ void admm_qp(const mpcqp_params& p, int b, double* __
       }
     }
   }
-  double* lf = st + state_lane_off(N);
-  lf[kFx * kWave + threadIdx.x] = act ? x : 0.0;
-  if (threadIdx.x == 0) {
-    double* sc = st + state_scal_off(N);
-    sc[1] = bad ? -1.0 : (ok ? 1.0 : 0.0);
-    sc[2] = (double)it;
-    sc[3] = (double)nfact;
+  if (dbg) {
+    dbg[state_lane_off(N) + kFx * kWave + threadIdx.x] = act ? x : 0.0;
+    if (threadIdx.x == 0) {
+      double* sc = dbg + state_scal_off(N);
+      sc[1] = bad ? -1.0 : (ok ? 1.0 : 0.0);
+      sc[2] = (double)it;
+      sc[3] = (double)nfact;
+    }
   }
+  x_out = act ? x : 0.0;
+  it_out = it;
+  nfact_out = nfact;
   T2.end(0);
   T.flush(0);   // g_stamps[0..3]: form, sweep, ADMM iteration body, termination checks
-  T2.flush(4);  // g_stamps[4]: whole k_admm
+  T2.flush(4);  // g_stamps[4]: whole ADMM phase
+  return bad ? -1 : (ok ? 1 : 0);
 }
 
 // ------------------------------------------------------------------ K2c: polish + outputs
 template <int N>
-__device__ __forceinline__ void finish_qp(const mpcqp_params& p, int b, const double* __restrict__ model,
-                                          const double* __restrict__ state, double* __restrict__ u0o,
-                                          double* __restrict__ Xo, double* __restrict__ Uo,
+__device__ __forceinline__ void finish_qp(const mpcqp_params& p, int b, const double* __restrict__ model, Ctx<N>& C,
+                                          double x_in, int admm_flag, int admm_it, int nfact,
+                                          double* __restrict__ u0o, double* __restrict__ Xo, double* __restrict__ Uo,
                                           int32_t* __restrict__ statuso, int32_t* __restrict__ iterso,
-                                          uint8_t* __restrict__ activeo, SolveSmem<N>& sm) {
+                                          uint8_t* __restrict__ activeo) {
   constexpr int n = 2 * N;
   const int lane = threadIdx.x;
-  const double* st = state + (size_t)b * state_stride(N);
-  Ctx<N> C;
-  C.load(st, lane, p.dt, sm.buf, sm.sv, sm.Dl, sm.P);
   const bool act = C.act;
   const bool use_admm = p.method == MPCQP_METHOD_ADMM;
   const bool do_polish = !use_admm || p.polish != 0;
-  const double* sc = st + state_scal_off(N);
-  const double admm_flag = sc[1];  // -1: non-finite data (k_setup) or ADMM numerical error
-  bool bad = admm_flag < 0.0;
-  const bool admm_ok = admm_flag > 0.0;
-  const int admm_it = use_admm ? (int)sc[2] : 0;
-  int nfact = use_admm ? (int)sc[3] : 0;
-  double x = use_admm ? st[state_lane_off(N) + kFx * kWave + lane] : 0.0;
+  bool bad = admm_flag < 0;  // non-finite data (setup) or ADMM numerical error
+  const bool admm_ok = admm_flag > 0;
+  double x = use_admm ? x_in : 0.0;
   const double x_admm = x;
   bool pol_ok = false;
   int pol_it = 0, n_ls = 0;
@@ -832,15 +862,13 @@ __device__ __forceinline__ void finish_qp(const mpcqp_params& p, int b, const do
 
 // ------------------------------------------------------------------ K2: fused solve
 // One wave runs its QP through setup -> ADMM -> polish/outputs without kernel boundaries, so
-// the batch drains once (the slowest QP's whole chain) instead of once per phase.  The phases
-// hand over through the per-QP state buffer (written and re-read by the same wave, so it stays
-// in this CU's caches) and share the LDS through a union.
-template <int N>
-union SolveLds {
-  SetupSmem<N> setup;
-  SolveSmem<N> solve;
-};
-
+// the batch drains once (the slowest QP's whole chain) instead of once per phase.  The scaled
+// problem never leaves the CU: Pbar stays in LDS, the per-lane data and the KKT inverse in
+// registers (the state buffer is written only when debug_state is set).
+// Occupancy: ~180 VGPRs (the KKT inverse is 2n of them) give 2 waves per SIMD.  Capping the
+// registers for a third wave (168, fits the ~13 KB of LDS at N = 20) measured no faster at
+// B = 4096: the four QPs per SIMD then run in 1.33 rounds instead of 2, but each wave shares
+// its SIMD's FP64 issue with two others.
 template <int N>
 __global__ __launch_bounds__(kWave) void k_solve(mpcqp_params p, int B, const uint8_t* __restrict__ mask,
                                                  const double* __restrict__ model, double* __restrict__ state,
@@ -850,13 +878,13 @@ __global__ __launch_bounds__(kWave) void k_solve(mpcqp_params p, int B, const ui
   __shared__ SolveLds<N> sm;
   const int b = blockIdx.x;
   if (b >= B || (mask && !mask[b])) return;
-  setup_qp<N>(p, b, model, state, sm.setup);
-  __syncthreads();
-  if (p.method == MPCQP_METHOD_ADMM) {
-    admm_qp<N>(p, b, state, sm.solve);
-    __syncthreads();
-  }
-  finish_qp<N>(p, b, model, state, u0o, Xo, Uo, statuso, iterso, activeo, sm.solve);
+  double* dbg = p.debug_state ? state + (size_t)b * state_stride(N) : nullptr;
+  Ctx<N> C;
+  const bool bad = setup_qp<N>(p, b, model, C, sm, state + (size_t)b * state_stride(N), dbg);
+  double x = 0.0;
+  int flag = bad ? -1 : 0, it = 0, nfact = 0;
+  if (p.method == MPCQP_METHOD_ADMM) flag = admm_qp<N>(p, C, bad, x, it, nfact, dbg);
+  finish_qp<N>(p, b, model, C, x, flag, it, nfact, u0o, Xo, Uo, statuso, iterso, activeo);
 }
 
 }  // namespace

@@ -47,6 +47,7 @@ DEFAULT_SOLVER_SETTINGS = dict(
     adaptive_rho_interval=25,
     polish=1,
     polish_max_iter=100,
+    debug_state=0,
 )
 
 
@@ -80,7 +81,7 @@ class MpcqpParams(ctypes.Structure):
         ("adaptive_rho_interval", ctypes.c_int32),
         ("polish", ctypes.c_int32),
         ("polish_max_iter", ctypes.c_int32),
-        ("reserved", ctypes.c_int32),
+        ("debug_state", ctypes.c_int32),
     ]
 
 

@@ -278,7 +278,7 @@ def test_setup_state_matches_restatement(cuda, N):
 
     batch = scenarios.config3(64, horizon=N)
     params = _params(N)
-    ctrl = BatchedMPCController(params, 64, device="cuda:0")
+    ctrl = BatchedMPCController(params, 64, device="cuda:0", debug_state=1)  # write the state buffer
     ctrl.solve_batch(batch.x0, batch.ref, batch.u_prev)
     torch.cuda.synchronize()
     L = _lib.lib()

@@ -1,0 +1,12 @@
+#!/bin/bash
+# Development: time every tools/diag/libmpcqp_*.so variant (config3 N=20) at B=512 and 4096.
+set -o pipefail
+mkdir -p gpurun_out
+for lib in tools/diag/libmpcqp_*.so; do
+  v=$(basename $lib .so); v=${v#libmpcqp_}
+  [ "$v" = stamps ] && continue
+  for B in 512 4096; do
+    MPCQP_LIB=$lib timeout -k 10 120 python bench.py --batch $B --steps 20 --warmup 3 --cpu-seconds 0 > gpurun_out/ab_${v}_$B.json || exit 1
+    python -c "import json; d=json.load(open('gpurun_out/ab_${v}_$B.json')); print('$v', $B, round(d['value']), round(d['kernel_ms']['k_solve'],4), d['solved_fraction'])"
+  done
+done

@@ -25,7 +25,9 @@ os.environ.setdefault("MPCQP_LIB", str(ROOT / "tools" / "diag" / "libmpcqp_stamp
 sys.path.insert(0, str(ROOT / "rrt-mpc_amd"))
 
 NAMES = {0: "admm.form", 1: "admm.sweep", 2: "admm.iteration", 3: "admm.check", 4: "admm.total",
-         8: "polish.form", 9: "polish.sweep", 10: "polish.solve", 11: "polish.linesearch", 12: "polish.total"}
+         8: "polish.form", 9: "polish.sweep", 10: "polish.solve", 11: "polish.linesearch", 12: "polish.total",
+         16: "setup.load_prefix", 17: "setup.condense", 18: "setup.unscaled", 19: "setup.ruiz", 20: "setup.write",
+         21: "setup.total"}
 
 
 def main() -> None:
@@ -47,7 +49,7 @@ def main() -> None:
     B = a.batch or b.size
     ctrl = BatchedMPCController(MPCConfig(horizon=b.horizon).to_parameters(0.8), max(B, b.size), device="cuda:0")
     L = _lib.lib()
-    buf = (ctypes.c_ulonglong * 16)()
+    buf = (ctypes.c_ulonglong * 32)()
     ctrl.solve_batch(x0, ref, up)
     torch.cuda.synchronize()
     if a.worst >= 0:
