@@ -143,9 +143,14 @@ struct Ctx {
       constexpr int k = decltype(kc)::value;
       double w[4];
       bcast<kNW>(r[k], w);
-      const double d = readlane(r[k], k);
+      // the pivot A[k][k] (lane k's r[k]) in every lane, straight from the row copy; then a
+      // vector reciprocal (v_rcp_f64 + two Newton steps, within an ulp of 1/d): no SGPR
+      // round trip and no IEEE division sequence on the step's critical path
+      const double d = dpp<0x150 + (k % 16)>(w[k / 16]);
       ok = ok && (d > 0.0) && isfinite(d);
-      const double inv = 1.0 / d;
+      double inv = __builtin_amdgcn_rcp(d);
+      inv = fma(inv, fma(-d, inv, 1.0), inv);
+      inv = fma(inv, fma(-d, inv, 1.0), inv);
       const bool piv = lane == k;
       const double ck = r[k] * inv;
       const double coef = piv ? inv - 1.0 : -ck;

@@ -99,6 +99,13 @@ __global__ __launch_bounds__(64) void k(const double* __restrict__ in, double* _
   if (lane == 0) cyc[blockIdx.x] = t1 - t0;
 }
 
+__global__ void k_spin(unsigned long long ticks, unsigned long long* out) {
+  const unsigned long long t0 = __builtin_amdgcn_s_memtime();
+  unsigned long long t = t0;
+  while (t - t0 < ticks) t = __builtin_amdgcn_s_memtime();
+  if (threadIdx.x == 0) out[0] = t - t0;
+}
+
 template <int V>
 void run(const char* name, double per, const double* din, double* dout, unsigned long long* dc, int waves, int grid) {
   hipLaunchKernelGGL(k<V>, dim3(grid), dim3(64), 0, 0, din, dout, dc, waves);
@@ -120,6 +127,19 @@ int main() {
   hipMalloc(&dout, sizeof(double) * 64 * 4096);
   hipMalloc(&dc, sizeof(unsigned long long) * 4096);
   hipMemcpy(din, h, sizeof h, hipMemcpyHostToDevice);
+  {  // s_memtime tick rate: spin 2e7 ticks, time with events
+    hipEvent_t e0, e1;
+    hipEventCreate(&e0);
+    hipEventCreate(&e1);
+    hipLaunchKernelGGL(k_spin, dim3(1), dim3(64), 0, 0, 1000000ull, dc);
+    hipEventRecord(e0);
+    hipLaunchKernelGGL(k_spin, dim3(1), dim3(64), 0, 0, 20000000ull, dc);
+    hipEventRecord(e1);
+    hipEventSynchronize(e1);
+    float ms;
+    hipEventElapsedTime(&ms, e0, e1);
+    printf("s_memtime: 2e7 ticks in %.3f ms -> %.3f GHz\n", ms, 2e7 / (ms * 1e-3) / 1e9);
+  }
   for (int waves : {1, 2048, 4096}) {
     run<0>("fma f64 dependent (per fma)", 16, din, dout, dc, waves, waves);
     run<1>("fma f64 4 chains (per fma)", 16, din, dout, dc, waves, waves);
