@@ -191,6 +191,24 @@ int mpcqp_fleet_step(mpcqp_ws* nominal, mpcqp_ws* relaxed, const mpcqp_fleet* f,
 int mpcqp_fleet_run(mpcqp_ws* nominal, mpcqp_ws* relaxed, const mpcqp_fleet* f, int steps, int use_graph,
                     void* stream);
 
+/*
+ * Batched build_reference: src/control/ref_builder.py:10-22 with
+ * src/common/geometry.py:9-45 (resample_polyline, heading_from_path, curvature_slowdown) for
+ * V polylines at once, one wave per polyline.  Inputs (device):
+ *   pts       P_total x 2      the polylines' points, concatenated
+ *   path_off  V + 1            polyline v = pts[path_off[v] .. path_off[v+1])
+ *   max_points                 >= every polyline's point count (LDS staging; at most 6144)
+ * Outputs (device):
+ *   ref       V x ref_stride x 4   rows [x, y, yaw, v] (the reference's xref, tail-padded)
+ *   ref_len   V                    rows written (>= horizon + 1; 0 for an empty polyline),
+ *                                  -(rows needed) when that exceeds ref_stride (nothing written),
+ *                                  MPCQP_REF_BAD_PATH when a polyline has more than max_points
+ * x and y follow numpy bit for bit given the same arc lengths; hypot and atan2 are the
+ * device's (within an ulp of the host libm), see tests/test_gpu_refbuild.py. */
+#define MPCQP_REF_BAD_PATH (-2147483647 - 1)
+int mpcqp_build_reference(int V, const double* pts, const int32_t* path_off, int max_points, double desired_speed,
+                          int horizon, double dt, int ref_stride, double* ref, int32_t* ref_len, void* stream);
+
 /* Workspace device buffers (for tests / inspection), layouts documented in DESIGN.md:
  *   model: K1 output, B x mpcqp_model_stride(N) doubles
  *   state: scaled QP + ADMM iterate (K2a/K2b output), B x mpcqp_state_stride(N) doubles */

@@ -108,6 +108,8 @@ def to_c_params(params, method: int = METHOD_ADMM, **settings) -> MpcqpParams:
     return c
 
 
+REF_BAD_PATH = -2147483648
+REF_MAX_POINTS = 6144
 FLEET_RUNNING = 0
 FLEET_GOAL = 1
 FLEET_ABORTED = 2
@@ -160,6 +162,9 @@ _SYMBOLS = {
                          ctypes.c_int),
     "mpcqp_fleet_run": ([ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(MpcqpFleet), ctypes.c_int, ctypes.c_int,
                          ctypes.c_void_p], ctypes.c_int),
+    "mpcqp_build_reference": ([ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_double,
+                               ctypes.c_int, ctypes.c_double, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
+                               ctypes.c_void_p], ctypes.c_int),
     "mpcqp_model_buffer": ([ctypes.c_void_p], ctypes.c_void_p),
     "mpcqp_model_stride": ([ctypes.c_int], ctypes.c_int),
     "mpcqp_state_buffer": ([ctypes.c_void_p], ctypes.c_void_p),
@@ -204,6 +209,8 @@ __all__ = [
     "MpcqpParams",
     "MpcqpFleet",
     "to_c_params",
+    "REF_BAD_PATH",
+    "REF_MAX_POINTS",
     "FLEET_RUNNING",
     "FLEET_GOAL",
     "FLEET_ABORTED",

@@ -18,4 +18,50 @@ def build_reference(path, desired_speed: float, horizon: int, dt: float) -> np.n
     return xref
 
 
-__all__ = ["build_reference"]
+def build_reference_batch(paths, desired_speed: float, horizon: int, dt: float, *, device=None,
+                          ref_stride: int | None = None, stream=None):
+    """``build_reference`` for many paths at once on the GPU (``mpcqp_build_reference``).
+
+    Returns ``(ref, ref_len)`` as device tensors: ``ref`` is ``(V, ref_stride, 4)`` float64 with
+    polyline ``v``'s reference in rows ``[0, ref_len[v])`` (identical to ``build_reference`` of that
+    path, up to an ulp of ``hypot``/``atan2``), ``ref_len`` is ``(V,)`` int32.  ``ref_stride``
+    defaults to an upper bound computed on the host from the path lengths.
+    """
+    import ctypes
+
+    import torch
+
+    from .. import _lib
+
+    if not torch.cuda.is_available():
+        raise _lib.LibraryError("build_reference_batch needs a ROCm GPU; there is no CPU fallback")
+    dev = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+    arrs = [np.asarray(p, dtype=float).reshape(-1, 2) for p in paths]
+    V = len(arrs)
+    counts = np.array([len(a) for a in arrs], dtype=np.int64)
+    off = np.zeros(V + 1, dtype=np.int32)
+    off[1:] = np.cumsum(counts)
+    max_points = int(counts.max()) if V else 0
+    if max_points > _lib.REF_MAX_POINTS:
+        raise ValueError(f"a path has {max_points} points; at most {_lib.REF_MAX_POINTS} are supported")
+    step = max(2.0, 0.8 * desired_speed * dt)
+    if ref_stride is None:  # resampled rows <= ceil(arc length / step) + 1, raw rows = points
+        arc = [float(np.hypot(*np.diff(a, axis=0).T).sum()) if len(a) > 1 else 0.0 for a in arrs]
+        bound = max([max(int(np.ceil(s / step)) + 2, len(a)) for s, a in zip(arc, arrs)], default=1)
+        ref_stride = max(bound, horizon + 1)
+    pts = torch.from_numpy(np.concatenate(arrs) if V and off[-1] else np.zeros((1, 2))).to(dev)
+    off_t = torch.from_numpy(off).to(dev)
+    ref = torch.empty((max(V, 1), ref_stride, 4), dtype=torch.float64, device=dev)
+    ref_len = torch.empty((max(V, 1),), dtype=torch.int32, device=dev)
+    if stream is None:
+        stream = torch.cuda.current_stream(dev)
+    L = _lib.lib()
+    with torch.cuda.device(dev):
+        _lib.check(L.mpcqp_build_reference(V, pts.data_ptr(), off_t.data_ptr(), max_points, float(desired_speed),
+                                           int(horizon), float(dt), int(ref_stride), ref.data_ptr(),
+                                           ref_len.data_ptr(), ctypes.c_void_p(stream.cuda_stream)),
+                   "mpcqp_build_reference")
+    return ref[:V], ref_len[:V]
+
+
+__all__ = ["build_reference", "build_reference_batch"]

@@ -19,7 +19,7 @@ from typing import List, Optional, Sequence
 import numpy as np
 
 from .. import _lib
-from ..control.ref_builder import build_reference
+from ..control.ref_builder import build_reference, build_reference_batch
 from .control_stage import TrackingResult
 
 PHASE_NAMES = {
@@ -148,16 +148,42 @@ class FleetTracker:
         self.max_steps = max_steps
 
     def reset_from_plans(self, paths: Sequence, starts: np.ndarray, goals: np.ndarray,
-                         max_steps: Optional[int] = None) -> List[np.ndarray]:
-        """``control_stage.py:69-87`` per vehicle: references from the planned paths, start states."""
-        refs, states = [], []
+                         max_steps: Optional[int] = None, *, device_reference: bool = False):
+        """``control_stage.py:69-87`` per vehicle: references from the planned paths, start states.
+
+        ``device_reference=True`` builds the references with the batched GPU ``build_reference``
+        (``mpcqp_build_reference``) straight into the fleet's buffers; otherwise on the host.
+        Returns the host references (or ``(ref, ref_len)`` device tensors)."""
+        states = []
         for path, start in zip(paths, starts):
             if not len(path):
                 raise RuntimeError("Planner returned an empty path")
-            refs.append(build_reference(path, self.mpc.v_px_s, self.horizon, self.mpc.dt))
             states.append(initial_state(path, start))
-        self.reset(refs, np.array(states).reshape(-1, 4), goals, max_steps)
+        states0 = np.array(states).reshape(-1, 4)
+        if device_reference:
+            ref, ref_len = build_reference_batch(paths, self.mpc.v_px_s, self.horizon, self.mpc.dt,
+                                                 device=self.device, ref_stride=self.max_ref_len)
+            self.reset_device(ref, ref_len, states0, goals, max_steps)
+            return ref, ref_len
+        refs = [build_reference(path, self.mpc.v_px_s, self.horizon, self.mpc.dt) for path in paths]
+        self.reset(refs, states0, goals, max_steps)
         return refs
+
+    def reset_device(self, ref, ref_len, states0: np.ndarray, goals: np.ndarray,
+                     max_steps: Optional[int] = None) -> None:
+        """Load references already on the device: ``ref`` (V, max_ref_len, 4) float64 and
+        ``ref_len`` (V,) int32 as produced by ``build_reference_batch``."""
+        torch = self._torch
+        V = int(ref.shape[0])
+        if int(ref.shape[1]) != self.max_ref_len:
+            raise ValueError(f"ref rows {int(ref.shape[1])} != max_ref_len {self.max_ref_len}")
+        lens = ref_len.cpu().numpy()
+        if V and (lens.min() < 1 or lens.max() > self.max_ref_len):
+            raise ValueError(f"reference lengths must be in [1, {self.max_ref_len}] (build_reference_batch "
+                             f"reports overflow as negative lengths)")
+        self.reset([np.zeros((1, 4))] * V, states0, goals, max_steps)
+        self._bufs["ref_global"][:V].copy_(ref)
+        self._bufs["ref_len"][:V].copy_(ref_len.to(torch.int32))
 
     # ------------------------------------------------------------------
     def step(self, steps: int = 1, stream=None) -> None:
