@@ -128,6 +128,31 @@ def config4(batch: int = 16384, horizon: int = 30, seed: int = 7) -> Batch:
                  f"config4_montecarlo_B{batch}_N{horizon}")
 
 
+def fleet5(vehicles: int = 100, seed: int = 5):
+    """Config-5-style fleet: V vehicles on RRT* tree branches of the default plan
+    (root -> random node of depth >= 3, Catmull-Rom smoothed as the planner does), start = branch
+    start + U(-3, 3) px, goal = branch end.  Returns (paths, starts (V, 2), goals (V, 2))."""
+    plan = load_default_plan()
+    nodes = plan["nodes"]
+    parent = nodes[:, 3].astype(int)
+    eligible = np.flatnonzero(_tree_depth(parent) >= 3)
+    rng = np.random.default_rng(seed)
+    cache: Dict[int, np.ndarray] = {}
+    paths = []
+    for _ in range(vehicles):
+        node = int(eligible[rng.integers(0, len(eligible))])
+        if node not in cache:
+            pts, j = [], node
+            while j >= 0:
+                pts.append(nodes[j, :2])
+                j = parent[j]
+            cache[node] = catmull_rom_spline(pts[::-1], samples_per_segment=20, alpha=0.5)
+        paths.append(cache[node])
+    starts = np.array([p[0] for p in paths]) + rng.uniform(-3, 3, size=(vehicles, 2))
+    goals = np.array([p[-1] for p in paths])
+    return paths, starts, goals
+
+
 CONFIGS = {"config2": config2, "config3": config3, "config4": config4}
 
-__all__ = ["Batch", "config2", "config3", "config4", "CONFIGS", "load_default_plan", "window"]
+__all__ = ["Batch", "config2", "config3", "config4", "fleet5", "CONFIGS", "load_default_plan", "window"]
