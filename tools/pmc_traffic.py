@@ -10,7 +10,7 @@ Units and corrections (MI355X_MICROARCH.md, HBM section):
     doubled (an upper bound for this kernel's 8-byte-per-lane reads; k_build, whose read
     bytes are known exactly, calibrates that access width and is reported beside it);
   * WRITE_SIZE is taken as is.
-k_solve = k_setup + k_admm + k_finish (one mpcqp_solve call).
+k_solve = the fused solve kernel (one dispatch per mpcqp_solve call).
 """
 from __future__ import annotations
 
@@ -20,7 +20,7 @@ import csv
 import json
 from pathlib import Path
 
-SOLVE = ("k_setup", "k_admm", "k_finish")
+SOLVE = ("k_solve",)
 
 
 def per_kernel(path: Path) -> dict:
@@ -65,9 +65,9 @@ def main() -> None:
                                           "fetch_bytes_raw": fetch["k_build"],
                                           "ratio": build_read_alg / fetch["k_build"]},
             "per_qp_bytes": (read + wr) / B,
-            "note": "FETCH doubled per the gfx950 correction; the solver's per-QP state (scaled "
-                    "Hessian etc., written by k_setup, re-read by k_admm and k_finish) dominates and "
-                    "stays Infinity-Cache resident, which these fabric-side counters still count",
+            "note": "FETCH doubled per the gfx950 correction (8-byte-per-lane loads: an upper bound, "
+                    "k_build calibrates that width); k_solve reads the 1.8 KB model per QP and "
+                    "writes the outputs; the scaled problem stays on chip",
         }
     }
     print(json.dumps(out, indent=1))
