@@ -209,6 +209,42 @@ int mpcqp_fleet_run(mpcqp_ws* nominal, mpcqp_ws* relaxed, const mpcqp_fleet* f, 
 int mpcqp_build_reference(int V, const double* pts, const int32_t* path_off, int max_points, double desired_speed,
                           int horizon, double dt, int ref_stride, double* ref, int32_t* ref_len, void* stream);
 
+/*
+ * Batched RRT* tree growth: RRTStarPlanner.plan's loop
+ * (src/planning/rrt_star.py:201-248, helpers :320-383) for V planning problems on one
+ * occupancy grid, one workgroup per problem.  The random samples of each problem's seed are
+ * drawn on the host with the reference's own numpy calls (_sample, :320-325) and passed in.
+ * Inputs (device):
+ *   occupancy  height x width uint8, row-major, 1 = free (the inflated grid)
+ *   start_goal V x 4          {start_x, start_y, goal_x, goal_y}
+ *   samples    V x max_iterations x 2   the sample of every iteration
+ * Outputs (device):
+ *   nodes      V x (max_iterations + 2) x 4   {x, y, cost, parent (-1 = root)} per tree node
+ *   count      V                   tree nodes (goal node included when reached)
+ *   meta       V x 2               {iterations run, goal index or -1}
+ */
+typedef struct mpcqp_rrt_params {
+  double step;            /* PlannerParameters.step (step_size, default 3) */
+  double goal_radius;     /* 10 */
+  double rewire_radius;   /* 20 */
+  double collision_step;  /* rrt_collision_step, 0.75 */
+  int32_t max_iterations; /* <= 5000 (LDS holds the tree) */
+  int32_t width;          /* occupancy.shape[1] */
+  int32_t height;         /* occupancy.shape[0] */
+  int32_t reserved;
+} mpcqp_rrt_params;
+
+int mpcqp_rrt_plan(const mpcqp_rrt_params* p, int V, const uint8_t* occupancy, const double* start_goal,
+                   const double* samples, double* nodes, int32_t* count, int32_t* meta, void* stream);
+
+/*
+ * Occupancy inflation: src/maps/inflate.py:18-51 (the fallback
+ * dilation the reference uses without OpenCV) for B grids of height x width uint8
+ * (1 = free, 0 = obstacle): out = 0 within the disk dx^2 + dy^2 <= r^2 of an obstacle.
+ * radius_px <= 0 copies.  Device pointers, out != occupancy.
+ */
+int mpcqp_inflate(int B, int height, int width, int radius_px, const uint8_t* occupancy, uint8_t* out, void* stream);
+
 /* Workspace device buffers (for tests / inspection), layouts documented in DESIGN.md:
  *   model: K1 output, B x mpcqp_model_stride(N) doubles
  *   state: scaled QP + ADMM iterate (K2a/K2b output), B x mpcqp_state_stride(N) doubles */

@@ -141,6 +141,24 @@ class MpcqpFleet(ctypes.Structure):
     ]
 
 
+class MpcqpRrtParams(ctypes.Structure):
+    """``mpcqp_rrt_params`` (include/mpcqp.h)."""
+
+    _fields_ = [
+        ("step", ctypes.c_double),
+        ("goal_radius", ctypes.c_double),
+        ("rewire_radius", ctypes.c_double),
+        ("collision_step", ctypes.c_double),
+        ("max_iterations", ctypes.c_int32),
+        ("width", ctypes.c_int32),
+        ("height", ctypes.c_int32),
+        ("reserved", ctypes.c_int32),
+    ]
+
+
+RRT_MAX_ITERATIONS = 5000
+
+
 class LibraryError(RuntimeError):
     pass
 
@@ -165,6 +183,8 @@ _SYMBOLS = {
     "mpcqp_build_reference": ([ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_double,
                                ctypes.c_int, ctypes.c_double, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
                                ctypes.c_void_p], ctypes.c_int),
+    "mpcqp_rrt_plan": ([ctypes.POINTER(MpcqpRrtParams), ctypes.c_int] + [ctypes.c_void_p] * 7, ctypes.c_int),
+    "mpcqp_inflate": ([ctypes.c_int] * 4 + [ctypes.c_void_p] * 3, ctypes.c_int),
     "mpcqp_model_buffer": ([ctypes.c_void_p], ctypes.c_void_p),
     "mpcqp_model_stride": ([ctypes.c_int], ctypes.c_int),
     "mpcqp_state_buffer": ([ctypes.c_void_p], ctypes.c_void_p),
@@ -208,6 +228,8 @@ def check(rc: int, what: str) -> None:
 __all__ = [
     "MpcqpParams",
     "MpcqpFleet",
+    "MpcqpRrtParams",
+    "RRT_MAX_ITERATIONS",
     "to_c_params",
     "REF_BAD_PATH",
     "REF_MAX_POINTS",

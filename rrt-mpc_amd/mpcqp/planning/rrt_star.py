@@ -1,0 +1,254 @@
+"""RRT* planning with the tree grown on the GPU: drop-in for ``src/planning/rrt_star.py``.
+
+``RRTStarPlanner(occupancy, params).plan(start, goal) -> PlanResult`` keeps the reference's
+names, arguments and results (``rrt_star.py:192-357``, ``plan_result.py``).  The expensive part,
+the tree growth loop (nearest / steer / segment checks / choose parent / rewire / goal,
+``:213-243``), runs in ``mpcqp_rrt_plan`` (``csrc/mpcqp_rrt.hip``), one workgroup per planning
+problem; ``BatchedRRTStarPlanner.plan_batch`` grows many trees at once (config 5: a fleet
+replanning).  The random stream of each problem is drawn here with the reference's own numpy
+calls (``_sample``, ``:320-325``) so every seed replays exactly; path extraction, shortcut
+pruning and Catmull-Rom smoothing (``:250-283``) are the reference's cheap host
+post-processing, restated below.
+"""
+from __future__ import annotations
+
+import ctypes
+import logging
+import math
+from dataclasses import dataclass, field
+from typing import List, Optional, Sequence, Tuple
+
+import numpy as np
+
+from .. import _lib
+from ..common.geometry import catmull_rom_spline
+
+LOG = logging.getLogger(__name__)
+
+
+@dataclass
+class PlannerParameters:
+    """``rrt_star.py:26-38``."""
+
+    step: float
+    goal_radius: float
+    max_iterations: int
+    rewire_radius: float
+    goal_sample_rate: float
+    random_seed: int
+    prune_path: bool = True
+    spline_samples: int = 20
+    spline_alpha: float = 0.5
+    dedupe_tolerance: float = 1e-9
+    collision_step: float = 1.0
+
+
+def default_planner_parameters(**overrides) -> PlannerParameters:
+    """``PlannerConfig().to_parameters()`` (``src/config.py:35-62``)."""
+    p = dict(step=3.0, goal_radius=10.0, max_iterations=2000, rewire_radius=20.0, goal_sample_rate=0.1,
+             random_seed=13, prune_path=True, spline_samples=20, spline_alpha=0.5, dedupe_tolerance=1e-9,
+             collision_step=0.75)
+    p.update(overrides)
+    return PlannerParameters(**p)
+
+
+@dataclass
+class RRTStarNode:
+    """``plan_result.py:8-15``."""
+
+    x: float
+    y: float
+    cost: float
+    parent: Optional[int]
+
+
+@dataclass
+class PlanResult:
+    """``plan_result.py:18-29``."""
+
+    success: bool
+    path: List[Tuple[float, float]]
+    nodes: List[RRTStarNode]
+    iterations: int
+    goal_index: Optional[int]
+    raw_path: Sequence[Tuple[float, float]] = field(default_factory=list)
+    pruned_path: Optional[Sequence[Tuple[float, float]]] = None
+    smoothed_path: Optional[Sequence[Tuple[float, float]]] = None
+
+
+def draw_samples(seed: int, goal, shape, goal_sample_rate: float, max_iterations: int) -> np.ndarray:
+    """The planner's sample of every iteration (``_sample``, ``rrt_star.py:320-325``): the same
+    ``numpy.random.default_rng(seed)`` calls in the same order (one per iteration, whether or
+    not the iteration then adds a node)."""
+    rng = np.random.default_rng(seed)
+    out = np.empty((max_iterations, 2))
+    h, w = int(shape[0]), int(shape[1])
+    gx, gy = float(goal[0]), float(goal[1])
+    for k in range(max_iterations):
+        if rng.random() < goal_sample_rate:
+            out[k] = (gx, gy)
+        else:
+            y = rng.integers(0, h)
+            x = rng.integers(0, w)
+            out[k] = (float(x), float(y))
+    return out
+
+
+def segment_is_free(occupancy: np.ndarray, start, end, collision_step: float) -> bool:
+    """``_segment_is_free`` (``rrt_star.py:339-352``), used by the host shortcut pruning."""
+    dx = end[0] - start[0]
+    dy = end[1] - start[1]
+    distance = math.hypot(dx, dy)
+    step = max(collision_step, 1e-3)
+    samples = max(1, int(math.ceil(distance / step)))
+    xs = np.linspace(start[0], end[0], samples + 1)
+    ys = np.linspace(start[1], end[1], samples + 1)
+    h, w = occupancy.shape
+    for x, y in zip(xs, ys):
+        xi = int(np.clip(round(x), 0, w - 1))
+        yi = int(np.clip(round(y), 0, h - 1))
+        if occupancy[yi, xi] == 0:
+            return False
+    return True
+
+
+def _finish(occupancy, params: PlannerParameters, nodes: List[RRTStarNode], iterations: int,
+            goal_index: Optional[int]) -> PlanResult:
+    """``rrt_star.py:245-294``: extract, shortcut-prune and smooth the path."""
+    success = goal_index is not None
+    raw_path: List[Tuple[float, float]] = []
+    pruned_path = None
+    smoothed_path = None
+    final_path: List[Tuple[float, float]] = []
+    if success:
+        idx = goal_index
+        while idx is not None:
+            raw_path.append((nodes[idx].x, nodes[idx].y))
+            idx = nodes[idx].parent
+        raw_path.reverse()
+        working = list(raw_path)
+        if params.prune_path and len(working) >= 2:
+            pruned = _shortcut_prune(occupancy, working, params.collision_step)
+            if len(pruned) >= 2:
+                pruned_path = pruned
+                working = pruned
+        if len(working) >= 2 and params.spline_samples > 1:
+            spline = catmull_rom_spline(working, samples_per_segment=params.spline_samples,
+                                        alpha=params.spline_alpha, dedupe_tol=params.dedupe_tolerance)
+            if len(spline) >= 2:
+                smoothed_path = [tuple(map(float, pt)) for pt in spline]
+                working = smoothed_path
+        final_path = [tuple(map(float, pt)) for pt in working]
+    else:
+        LOG.warning("Failed to find a path within %d iterations", params.max_iterations)
+    return PlanResult(
+        success=success,
+        path=final_path,
+        nodes=nodes,
+        iterations=iterations,
+        goal_index=goal_index,
+        raw_path=[tuple(map(float, pt)) for pt in raw_path],
+        pruned_path=None if pruned_path is None else [tuple(map(float, pt)) for pt in pruned_path],
+        smoothed_path=smoothed_path,
+    )
+
+
+def _shortcut_prune(occupancy, path, collision_step) -> List[Tuple[float, float]]:
+    """``rrt_star.py:376-389``."""
+    if len(path) <= 2:
+        return list(path)
+    pts = [tuple(map(float, pt)) for pt in path]
+    pruned = [pts[0]]
+    i = 0
+    while i < len(pts) - 1:
+        j = len(pts) - 1
+        while j > i + 1 and not segment_is_free(occupancy, pts[i], pts[j], collision_step):
+            j -= 1
+        pruned.append(pts[j])
+        i = j
+    return pruned
+
+
+class BatchedRRTStarPlanner:
+    """Grow V RRT* trees on one occupancy grid at once on the GPU."""
+
+    def __init__(self, occupancy: np.ndarray, params: PlannerParameters, *, device=None) -> None:
+        import torch
+
+        if not torch.cuda.is_available():
+            raise _lib.LibraryError("BatchedRRTStarPlanner needs a ROCm GPU; there is no CPU fallback")
+        if not 1 <= int(params.max_iterations) <= _lib.RRT_MAX_ITERATIONS:
+            raise ValueError(f"max_iterations must be in [1, {_lib.RRT_MAX_ITERATIONS}]")
+        self._torch = torch
+        self.occupancy = np.ascontiguousarray(occupancy, dtype=np.uint8)
+        self.params = params
+        self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+        self._occ = torch.from_numpy(self.occupancy).to(self.device)
+        c = _lib.MpcqpRrtParams()
+        c.step = float(params.step)
+        c.goal_radius = float(params.goal_radius)
+        c.rewire_radius = float(params.rewire_radius)
+        c.collision_step = float(params.collision_step)
+        c.max_iterations = int(params.max_iterations)
+        c.height, c.width = (int(v) for v in self.occupancy.shape)
+        self._c = c
+
+    def grow(self, starts, goals, seeds, stream=None):
+        """Launch the tree growth; returns device tensors (nodes (V, M, 4), count (V,), meta (V, 2))."""
+        torch = self._torch
+        starts = np.asarray(starts, dtype=float).reshape(-1, 2)
+        goals = np.asarray(goals, dtype=float).reshape(-1, 2)
+        V = len(starts)
+        T = int(self.params.max_iterations)
+        samples = np.stack([draw_samples(int(s), g, self.occupancy.shape, self.params.goal_sample_rate, T)
+                            for s, g in zip(seeds, goals)]) if V else np.zeros((1, T, 2))
+        dev = self.device
+        sg = torch.from_numpy(np.hstack([starts, goals]) if V else np.zeros((1, 4))).to(dev)
+        smp = torch.from_numpy(samples).to(dev)
+        nodes = torch.empty((max(V, 1), T + 2, 4), dtype=torch.float64, device=dev)
+        count = torch.empty((max(V, 1),), dtype=torch.int32, device=dev)
+        meta = torch.empty((max(V, 1), 2), dtype=torch.int32, device=dev)
+        if stream is None:
+            stream = torch.cuda.current_stream(dev)
+        L = _lib.lib()
+        with torch.cuda.device(dev):
+            _lib.check(L.mpcqp_rrt_plan(ctypes.byref(self._c), V, self._occ.data_ptr(), sg.data_ptr(),
+                                        smp.data_ptr(), nodes.data_ptr(), count.data_ptr(), meta.data_ptr(),
+                                        ctypes.c_void_p(stream.cuda_stream)), "mpcqp_rrt_plan")
+        return nodes[:V], count[:V], meta[:V]
+
+    def plan_batch(self, starts, goals, seeds=None) -> List[PlanResult]:
+        """``plan(start, goal)`` for every problem (seed defaults to ``params.random_seed``)."""
+        starts = np.asarray(starts, dtype=float).reshape(-1, 2)
+        V = len(starts)
+        if seeds is None:
+            seeds = [self.params.random_seed] * V
+        nodes, count, meta = self.grow(starts, goals, seeds)
+        nodes = nodes.cpu().numpy()
+        count = count.cpu().numpy()
+        meta = meta.cpu().numpy()
+        out = []
+        for v in range(V):
+            tree = [RRTStarNode(float(x), float(y), float(c), None if p < 0 else int(p))
+                    for x, y, c, p in nodes[v, : count[v]]]
+            gi = int(meta[v, 1])
+            out.append(_finish(self.occupancy, self.params, tree, int(meta[v, 0]), None if gi < 0 else gi))
+        return out
+
+
+class RRTStarPlanner:
+    """Compute paths on an inflated occupancy grid (``rrt_star.py:192-357``); the tree grows
+    on the GPU."""
+
+    def __init__(self, occupancy: np.ndarray, params: PlannerParameters) -> None:
+        self.occupancy = occupancy
+        self.params = params
+
+    def plan(self, start: Tuple[float, float], goal: Tuple[float, float]) -> PlanResult:
+        LOG.info("Running RRT* planner from %s to %s (max_iterations=%d)", start, goal, self.params.max_iterations)
+        planner = BatchedRRTStarPlanner(self.occupancy, self.params)
+        return planner.plan_batch([start], [goal], [self.params.random_seed])[0]
+
+
+__all__ = ["PlannerParameters", "RRTStarNode", "PlanResult", "RRTStarPlanner", "BatchedRRTStarPlanner",
+           "draw_samples", "segment_is_free", "default_planner_parameters"]

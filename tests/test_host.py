@@ -40,7 +40,8 @@ def test_library_exports_every_header_symbol():
     assert L.mpcqp_model_stride(20) % 8 == 0
 
 
-@pytest.mark.parametrize("cls_name,c_name", [("MpcqpParams", "mpcqp_params"), ("MpcqpFleet", "mpcqp_fleet")])
+@pytest.mark.parametrize("cls_name,c_name", [("MpcqpParams", "mpcqp_params"), ("MpcqpFleet", "mpcqp_fleet"),
+                                             ("MpcqpRrtParams", "mpcqp_rrt_params")])
 def test_struct_layout_matches_c(tmp_path, cls_name, c_name):
     """ctypes mirrors of mpcqp_params / mpcqp_fleet == the C compiler's layout (sizeof, offsets)."""
     from mpcqp import _lib

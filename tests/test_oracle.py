@@ -131,3 +131,31 @@ def test_c_restatement_unwrap_is_numpy_bit_exact(golden):
         yaw = out["model"][0, 7 * N + 2: 7 * N + 2 + 4 * (N + 1): 4]
         np.testing.assert_array_equal(yaw, g["unwrapped"][i, :L])
     assert p.horizon == 30
+
+
+def test_rrt_oracle_reproduces_reference_trees(golden):
+    """oracle/rrt_oracle.grow_tree with the planner's own sample stream == the reference's
+    RRTStarPlanner trees (planning.npz, generated from the reference), bit for bit."""
+    import rrt_oracle as ro
+    from mpcqp.planning.rrt_star import default_planner_parameters, draw_samples
+
+    g = golden("planning.npz")
+    occ = g["rrt_occupancy"]
+    prm = default_planner_parameters()
+    for k in range(5):
+        sx, sy, gx, gy, seed, iters = g[f"rrt{k}_case"]
+        smp = draw_samples(int(seed), (gx, gy), occ.shape, prm.goal_sample_rate, int(iters))
+        nodes, it, gi = ro.grow_tree(occ, (sx, sy), (gx, gy), smp, step=prm.step, goal_radius=prm.goal_radius,
+                                     rewire_radius=prm.rewire_radius, collision_step=prm.collision_step)
+        np.testing.assert_array_equal(nodes, g[f"rrt{k}_nodes"])
+        assert [int(g[f"rrt{k}_meta"][0]), it, gi] == [int(gi >= 0), *map(int, g[f"rrt{k}_meta"][1:])]
+
+
+def test_inflation_oracle_reproduces_reference(golden):
+    import rrt_oracle as ro
+
+    g = golden("planning.npz")
+    np.testing.assert_array_equal(ro.dilate(g["inflate_default_in"], int(g["inflate_default_radius"])),
+                                  g["inflate_default_out"])
+    for k, r in enumerate(g["inflate_random_radius"]):
+        np.testing.assert_array_equal(ro.dilate(g["inflate_random_in"][k], int(r)), g["inflate_random_out"][k])
