@@ -212,12 +212,14 @@ int mpcqp_build_reference(int V, const double* pts, const int32_t* path_off, int
 /*
  * Batched RRT* tree growth: RRTStarPlanner.plan's loop
  * (src/planning/rrt_star.py:201-248, helpers :320-383) for V planning problems on one
- * occupancy grid, one workgroup per problem.  The random samples of each problem's seed are
- * drawn on the host with the reference's own numpy calls (_sample, :320-325) and passed in.
+ * occupancy grid, one workgroup per problem.  The random samples (_sample, :320-325) replay
+ * each problem's numpy stream exactly, from one of:
+ *   samples    V x max_iterations x 2   drawn on the host, or NULL to draw on the device from
+ *   rng_state  V x 4 uint64             numpy.random.default_rng(seed).bit_generator.state:
+ *                                       {state lo, state hi, inc lo, inc hi} (PCG64)
  * Inputs (device):
- *   occupancy  height x width uint8, row-major, 1 = free (the inflated grid)
+ *   occupancy  height x width uint8, row-major, 1 = free (the inflated grid), at least 2 x 2
  *   start_goal V x 4          {start_x, start_y, goal_x, goal_y}
- *   samples    V x max_iterations x 2   the sample of every iteration
  * Outputs (device):
  *   nodes      V x (max_iterations + 2) x 4   {x, y, cost, parent (-1 = root)} per tree node
  *   count      V                   tree nodes (goal node included when reached)
@@ -228,6 +230,7 @@ typedef struct mpcqp_rrt_params {
   double goal_radius;     /* 10 */
   double rewire_radius;   /* 20 */
   double collision_step;  /* rrt_collision_step, 0.75 */
+  double goal_sample_rate; /* 0.1 (device sampling) */
   int32_t max_iterations; /* <= 5000 (LDS holds the tree) */
   int32_t width;          /* occupancy.shape[1] */
   int32_t height;         /* occupancy.shape[0] */
@@ -235,7 +238,8 @@ typedef struct mpcqp_rrt_params {
 } mpcqp_rrt_params;
 
 int mpcqp_rrt_plan(const mpcqp_rrt_params* p, int V, const uint8_t* occupancy, const double* start_goal,
-                   const double* samples, double* nodes, int32_t* count, int32_t* meta, void* stream);
+                   const double* samples, const uint64_t* rng_state, double* nodes, int32_t* count, int32_t* meta,
+                   void* stream);
 
 /*
  * Occupancy inflation: src/maps/inflate.py:18-51 (the fallback

@@ -12,9 +12,11 @@
 //                  through the new node and has a free segment from it          (:374-383)
 //   goal           within goal_radius and a free segment -> goal node appended  (:234-243)
 // The per-iteration scans over the tree run across the 256 threads; the tree (x, y, cost,
-// parent) lives in LDS.  The random samples (:320-325) are drawn on the host with the
-// reference's own numpy calls (mpcqp/planning/rrt_star.py) and passed in, so every problem
-// replays its seed's stream exactly.  Arithmetic is uncontracted; hypot / atan2 / sin / cos
+// parent) lives in LDS.  The random samples (:320-325) replay numpy's stream exactly: either
+// drawn on the host and passed in, or drawn here from each problem's PCG64 state (numpy's
+// generator: 128-bit LCG step, XSL-RR output; random() = (next64 >> 11) * 2^-53;
+// integers(0, n) = Lemire's bounded draw on next32, which hands out the two halves of one
+// next64 in turn -- numpy's has_uint32 buffer).  Arithmetic is uncontracted; hypot / atan2 / sin / cos
 // are the device's (within an ulp of the host libm).
 #include "mpcqp_common.h"
 
@@ -55,6 +57,45 @@ struct PlanSmem {
   double red_d[kPlanWaves];
   int red_i[kPlanWaves];
   int flag;
+  double qx, qy;  // this iteration's sample (device sampling)
+};
+
+// numpy's PCG64 (bit_generator.state: state, inc) and the Generator draws _sample makes
+struct Pcg64 {
+  unsigned __int128 s, inc;
+  int has32;
+  uint32_t u32;
+  __device__ uint64_t next64() {
+    const unsigned __int128 mult = ((unsigned __int128)0x2360ED051FC65DA4ull << 64) | 0x4385DF649FCCF645ull;
+    s = s * mult + inc;
+    const uint64_t hi = (uint64_t)(s >> 64), lo = (uint64_t)s;
+    const uint64_t x = hi ^ lo;
+    const unsigned r = (unsigned)(s >> 122);
+    return (x >> r) | (x << ((64u - r) & 63u));
+  }
+  __device__ uint32_t next32() {
+    if (has32) {
+      has32 = 0;
+      return u32;
+    }
+    const uint64_t v = next64();
+    has32 = 1;
+    u32 = (uint32_t)(v >> 32);
+    return (uint32_t)v;
+  }
+  __device__ double random() { return (double)(next64() >> 11) * (1.0 / 9007199254740992.0); }
+  __device__ uint32_t bounded(uint32_t n) {  // integers(0, n), n >= 2
+    uint64_t m = (uint64_t)next32() * n;
+    uint32_t left = (uint32_t)m;
+    if (left < n) {
+      const uint32_t thr = (uint32_t)(0u - n) % n;
+      while (left < thr) {
+        m = (uint64_t)next32() * n;
+        left = (uint32_t)m;
+      }
+    }
+    return (uint32_t)(m >> 32);
+  }
 };
 
 // block argmin of (v, i): smallest v, then smallest i
@@ -96,6 +137,7 @@ __device__ bool block_all(bool ok, PlanSmem& s) {
 __global__ __launch_bounds__(kPlanThreads) void k_rrt_plan(mpcqp_rrt_params p, int V, const uint8_t* __restrict__ occ,
                                                             const double* __restrict__ start_goal,
                                                             const double* __restrict__ samples,
+                                                            const uint64_t* __restrict__ rng_state,
                                                             double* __restrict__ nodes_out, int32_t* __restrict__ count_out,
                                                             int32_t* __restrict__ meta_out) {
 #pragma clang fp contract(off)
@@ -120,10 +162,37 @@ __global__ __launch_bounds__(kPlanThreads) void k_rrt_plan(mpcqp_rrt_params p, i
   }
   __syncthreads();
   int count = 1, goal_index = -1, iterations = 0;
-  const double* smp = samples + (size_t)v * p.max_iterations * 2;
+  const double* smp = samples ? samples + (size_t)v * p.max_iterations * 2 : nullptr;
+  Pcg64 rng{};
+  if (!smp && tid == 0) {
+    const uint64_t* r = rng_state + 4 * (size_t)v;  // {state lo, state hi, inc lo, inc hi}
+    rng.s = ((unsigned __int128)r[1] << 64) | r[0];
+    rng.inc = ((unsigned __int128)r[3] << 64) | r[2];
+    rng.has32 = 0;
+    rng.u32 = 0;
+  }
   for (int it = 1; it <= p.max_iterations; ++it) {
     iterations = it;
-    const double qx = smp[2 * (it - 1)], qy = smp[2 * (it - 1) + 1];
+    double qx, qy;
+    if (smp) {
+      qx = smp[2 * (it - 1)];
+      qy = smp[2 * (it - 1) + 1];
+    } else {  // _sample (rrt_star.py:320-325): one draw sequence per iteration, kept or not
+      if (tid == 0) {
+        if (rng.random() < p.goal_sample_rate) {
+          sm.qx = gx;
+          sm.qy = gy;
+        } else {
+          const uint32_t yy = rng.bounded((uint32_t)p.height);
+          const uint32_t xx = rng.bounded((uint32_t)p.width);
+          sm.qx = (double)xx;
+          sm.qy = (double)yy;
+        }
+      }
+      __syncthreads();
+      qx = sm.qx;
+      qy = sm.qy;
+    }
     // nearest (np.argmin: first minimum)
     double bd = INFINITY;
     int bi = 0x7fffffff;
@@ -215,14 +284,16 @@ __global__ __launch_bounds__(kPlanThreads) void k_rrt_plan(mpcqp_rrt_params p, i
 extern "C" {
 
 int mpcqp_rrt_plan(const mpcqp_rrt_params* p, int V, const uint8_t* occupancy, const double* start_goal,
-                   const double* samples, double* nodes, int32_t* count, int32_t* meta, void* stream) {
+                   const double* samples, const uint64_t* rng_state, double* nodes, int32_t* count, int32_t* meta,
+                   void* stream) {
   if (!p) return fail(MPCQP_E_ARG, "null params");
   if (V < 0) return fail(MPCQP_E_ARG, "V must be >= 0");
   if (V == 0) return MPCQP_OK;
-  if (!occupancy || !start_goal || !samples || !nodes || !count || !meta) return fail(MPCQP_E_ARG, "null argument");
+  if (!occupancy || !start_goal || !nodes || !count || !meta) return fail(MPCQP_E_ARG, "null argument");
+  if (!samples && !rng_state) return fail(MPCQP_E_ARG, "need samples or rng_state");
   if (p->max_iterations < 1 || p->max_iterations > kMaxPlanIterations)
     return fail(MPCQP_E_ARG, "max_iterations outside [1, " + std::to_string(kMaxPlanIterations) + "]");
-  if (p->width < 1 || p->height < 1) return fail(MPCQP_E_ARG, "empty grid");
+  if (p->width < 2 || p->height < 2) return fail(MPCQP_E_ARG, "grid must be at least 2 x 2");
   if (!(p->step > 0.0) || !(p->rewire_radius >= 0.0) || !(p->goal_radius >= 0.0) || !(p->collision_step >= 0.0))
     return fail(MPCQP_E_ARG, "bad planner parameters");
   const size_t lds = (size_t)(p->max_iterations + 2) * (3 * sizeof(double) + sizeof(int));
@@ -233,7 +304,7 @@ int mpcqp_rrt_plan(const mpcqp_rrt_params* p, int V, const uint8_t* occupancy, c
     if (e != hipSuccess) return fail(MPCQP_E_HIP, std::string("hipFuncSetAttribute: ") + hipGetErrorString(e));
   }
   hipLaunchKernelGGL(k_rrt_plan, dim3(V), dim3(kPlanThreads), lds_r, static_cast<hipStream_t>(stream), *p, V,
-                     occupancy, start_goal, samples, nodes, count, meta);
+                     occupancy, start_goal, samples, rng_state, nodes, count, meta);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return fail(MPCQP_E_HIP, std::string("k_rrt_plan launch: ") + hipGetErrorString(e));
   return MPCQP_OK;

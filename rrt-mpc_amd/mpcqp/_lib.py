@@ -149,6 +149,7 @@ class MpcqpRrtParams(ctypes.Structure):
         ("goal_radius", ctypes.c_double),
         ("rewire_radius", ctypes.c_double),
         ("collision_step", ctypes.c_double),
+        ("goal_sample_rate", ctypes.c_double),
         ("max_iterations", ctypes.c_int32),
         ("width", ctypes.c_int32),
         ("height", ctypes.c_int32),
@@ -183,7 +184,7 @@ _SYMBOLS = {
     "mpcqp_build_reference": ([ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_double,
                                ctypes.c_int, ctypes.c_double, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
                                ctypes.c_void_p], ctypes.c_int),
-    "mpcqp_rrt_plan": ([ctypes.POINTER(MpcqpRrtParams), ctypes.c_int] + [ctypes.c_void_p] * 7, ctypes.c_int),
+    "mpcqp_rrt_plan": ([ctypes.POINTER(MpcqpRrtParams), ctypes.c_int] + [ctypes.c_void_p] * 8, ctypes.c_int),
     "mpcqp_inflate": ([ctypes.c_int] * 4 + [ctypes.c_void_p] * 3, ctypes.c_int),
     "mpcqp_model_buffer": ([ctypes.c_void_p], ctypes.c_void_p),
     "mpcqp_model_stride": ([ctypes.c_int], ctypes.c_int),

@@ -94,6 +94,20 @@ def draw_samples(seed: int, goal, shape, goal_sample_rate: float, max_iterations
     return out
 
 
+def pcg64_states(seeds) -> np.ndarray:
+    """``numpy.random.default_rng(seed).bit_generator.state`` per seed as (V, 4) uint64
+    {state lo, state hi, inc lo, inc hi}: the device draws _sample's stream from it."""
+    m = (1 << 64) - 1
+    out = np.empty((len(seeds), 4), dtype=np.uint64)
+    for i, sd in enumerate(seeds):
+        st = np.random.default_rng(int(sd)).bit_generator.state
+        if st["bit_generator"] != "PCG64":
+            raise RuntimeError("numpy's default generator is no longer PCG64")
+        s, inc = st["state"]["state"], st["state"]["inc"]
+        out[i] = (s & m, s >> 64, inc & m, inc >> 64)
+    return out
+
+
 def segment_is_free(occupancy: np.ndarray, start, end, collision_step: float) -> bool:
     """``_segment_is_free`` (``rrt_star.py:339-352``), used by the host shortcut pruning."""
     dx = end[0] - start[0]
@@ -189,22 +203,30 @@ class BatchedRRTStarPlanner:
         c.goal_radius = float(params.goal_radius)
         c.rewire_radius = float(params.rewire_radius)
         c.collision_step = float(params.collision_step)
+        c.goal_sample_rate = float(params.goal_sample_rate)
         c.max_iterations = int(params.max_iterations)
         c.height, c.width = (int(v) for v in self.occupancy.shape)
         self._c = c
 
-    def grow(self, starts, goals, seeds, stream=None):
-        """Launch the tree growth; returns device tensors (nodes (V, M, 4), count (V,), meta (V, 2))."""
+    def grow(self, starts, goals, seeds, stream=None, *, host_samples: bool = False):
+        """Launch the tree growth; returns device tensors (nodes (V, M, 4), count (V,), meta (V, 2)).
+
+        The samples replay ``numpy.random.default_rng(seed)``: drawn on the device from the
+        generator's PCG64 state (default), or with ``host_samples=True`` by numpy itself."""
         torch = self._torch
         starts = np.asarray(starts, dtype=float).reshape(-1, 2)
         goals = np.asarray(goals, dtype=float).reshape(-1, 2)
         V = len(starts)
         T = int(self.params.max_iterations)
-        samples = np.stack([draw_samples(int(s), g, self.occupancy.shape, self.params.goal_sample_rate, T)
-                            for s, g in zip(seeds, goals)]) if V else np.zeros((1, T, 2))
         dev = self.device
         sg = torch.from_numpy(np.hstack([starts, goals]) if V else np.zeros((1, 4))).to(dev)
-        smp = torch.from_numpy(samples).to(dev)
+        smp = rs = None
+        if host_samples:
+            samples = np.stack([draw_samples(int(s), g, self.occupancy.shape, self.params.goal_sample_rate, T)
+                                for s, g in zip(seeds, goals)]) if V else np.zeros((1, T, 2))
+            smp = torch.from_numpy(samples).to(dev)
+        else:
+            rs = torch.from_numpy(pcg64_states(seeds) if V else np.zeros((1, 4), np.uint64)).to(dev)
         nodes = torch.empty((max(V, 1), T + 2, 4), dtype=torch.float64, device=dev)
         count = torch.empty((max(V, 1),), dtype=torch.int32, device=dev)
         meta = torch.empty((max(V, 1), 2), dtype=torch.int32, device=dev)
@@ -213,8 +235,9 @@ class BatchedRRTStarPlanner:
         L = _lib.lib()
         with torch.cuda.device(dev):
             _lib.check(L.mpcqp_rrt_plan(ctypes.byref(self._c), V, self._occ.data_ptr(), sg.data_ptr(),
-                                        smp.data_ptr(), nodes.data_ptr(), count.data_ptr(), meta.data_ptr(),
-                                        ctypes.c_void_p(stream.cuda_stream)), "mpcqp_rrt_plan")
+                                        None if smp is None else smp.data_ptr(),
+                                        None if rs is None else rs.data_ptr(), nodes.data_ptr(), count.data_ptr(),
+                                        meta.data_ptr(), ctypes.c_void_p(stream.cuda_stream)), "mpcqp_rrt_plan")
         return nodes[:V], count[:V], meta[:V]
 
     def plan_batch(self, starts, goals, seeds=None) -> List[PlanResult]:
@@ -251,4 +274,4 @@ class RRTStarPlanner:
 
 
 __all__ = ["PlannerParameters", "RRTStarNode", "PlanResult", "RRTStarPlanner", "BatchedRRTStarPlanner",
-           "draw_samples", "segment_is_free", "default_planner_parameters"]
+           "draw_samples", "pcg64_states", "segment_is_free", "default_planner_parameters"]

@@ -1,0 +1,104 @@
+#!/usr/bin/env python3
+"""BASELINE config 5 on one GPU: V vehicles on the default inflated 80x80 grid, each planned
+with RRT* (batched, GPU), tracked in closed loop with MPC (fleet, GPU) and re-planned by the
+trigger of mpcqp/pipeline/swarm.py.  Also times the planner alone (trees/s, batched GPU vs the
+reference algorithm restated in Python on one host core) and the inflation kernel.
+
+    python tools/swarm_bench.py [--vehicles 100 1024] [--steps 300]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import sys
+import time
+from pathlib import Path
+
+import numpy as np
+
+ROOT = Path(__file__).resolve().parents[1]
+sys.path.insert(0, str(ROOT / "rrt-mpc_amd"))
+sys.path.insert(0, str(ROOT / "oracle"))
+
+
+def pairs(occ, V, seed):
+    rng = np.random.default_rng(seed)
+    free = np.argwhere(occ == 1)
+    s, g = [], []
+    while len(s) < V:
+        a, b = free[rng.integers(0, len(free), 2)]
+        if np.hypot(*(a - b)) > 30:
+            s.append(a[::-1].astype(float))
+            g.append(b[::-1].astype(float))
+    return np.array(s), np.array(g)
+
+
+def main() -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--vehicles", type=int, nargs="+", default=[100, 1024])
+    ap.add_argument("--steps", type=int, default=300)
+    a = ap.parse_args()
+    import torch
+
+    from mpcqp.config import MPCConfig
+    from mpcqp.maps.inflate import inflate_binary_occupancy
+    from mpcqp.pipeline.swarm import Swarm
+    from mpcqp.planning.rrt_star import BatchedRRTStarPlanner, default_planner_parameters, draw_samples
+
+    d = np.load(ROOT / "rrt-mpc_amd" / "mpcqp" / "data" / "default_plan.npz")
+    occ = d["occupancy"]
+    out = {"grid": list(occ.shape), "runs": []}
+    prm = default_planner_parameters()
+    for V in a.vehicles:
+        starts, goals = pairs(occ, V, 5)
+        sw = Swarm(occ, MPCConfig(horizon=15, sim_steps=a.steps), prm, map_resolution=0.8, max_vehicles=V,
+                   device="cuda:0", replan_distance=15.0)
+        sw.run(starts[:4], goals[:4], seeds=np.arange(4), sim_steps=5)  # warm
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        res = sw.run(starts, goals, seeds=np.arange(V), check_every=25)
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+        run = {"vehicles": V, "seconds": dt, "vehicle_steps": int(res.steps.sum()),
+               "planned": int(res.planned.sum()), "goal_reached": int((res.phase == 1).sum()),
+               "replans": int(res.replans.sum()), **{k: round(v, 4) for k, v in res.timings.items()}}
+        out["runs"].append(run)
+        print(json.dumps(run), flush=True)
+    # planner alone: batched GPU tree growth vs the reference algorithm in Python (one core)
+    import rrt_oracle as ro
+
+    for V in (1, 100, 1024):
+        starts, goals = pairs(occ, V, 9)
+        pl = BatchedRRTStarPlanner(occ, prm, device="cuda:0")
+        pl.grow(starts[:1], goals[:1], [0])
+        smp_t0 = time.perf_counter()
+        pl.grow(starts, goals, np.arange(V))
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - smp_t0
+        out.setdefault("planner", []).append({"trees": V, "seconds": dt, "trees_per_s": V / dt,
+                                              "note": "device-side sampling from each seed's numpy PCG64 state; host post-processing excluded"})
+        print(json.dumps(out["planner"][-1]), flush=True)
+    starts, goals = pairs(occ, 8, 9)
+    t0 = time.perf_counter()
+    for v in range(8):
+        smp = draw_samples(v, goals[v], occ.shape, prm.goal_sample_rate, prm.max_iterations)
+        ro.grow_tree(occ, starts[v], goals[v], smp, step=prm.step, goal_radius=prm.goal_radius,
+                     rewire_radius=prm.rewire_radius, collision_step=prm.collision_step)
+    dt = time.perf_counter() - t0
+    out["planner_cpu_reference_algorithm"] = {"trees": 8, "seconds": dt, "trees_per_s": 8 / dt, "cores": 1}
+    # inflation: 64 grids of 1024x1024, radius 5
+    g = (torch.rand((64, 1024, 1024), device="cuda:0") > 0.01).to(torch.uint8)
+    inflate_binary_occupancy(g, 5)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(5):
+        inflate_binary_occupancy(g, 5)
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / 5
+    out["inflate"] = {"grids": 64, "cells": 64 * 1024 * 1024, "radius": 5, "seconds": dt,
+                      "gcells_per_s": 64 * 1024 * 1024 / dt / 1e9}
+    print(json.dumps(out))
+
+
+if __name__ == "__main__":
+    main()
