@@ -325,16 +325,6 @@ static void condense(const mpcqp_params* p, const double* model, qp_t* s) {
   }
 }
 
-/* scaled objective 0.5 x'Px + q'x + sum w dist(Cx,[l,u])^2 given Px */
-static double pen(const qp_t* s, const double* z) {
-  double t = 0.0;
-  for (int r = 0; r < s->m; ++r) {
-    double d = z[r] > s->u[r] ? z[r] - s->u[r] : (z[r] < s->l[r] ? s->l[r] - z[r] : 0.0);
-    t += s->w[r] * d * d;
-  }
-  return t;
-}
-
 static void codes_of(const qp_t* s, const double* z, uint8_t* cd) {
   for (int r = 0; r < s->m; ++r) cd[r] = z[r] > s->u[r] ? 2 : (z[r] < s->l[r] ? 1 : 0);
 }
@@ -584,9 +574,11 @@ void mpcqp_cpu_solve_one(const mpcqp_params* p, const double* model, double* u0,
     int pol_ok = 0;
     uint8_t cd[MAXR], cn[MAXR];
     double zc[MAXR], rw[MAXR], tmp[MAXR], rhs[MAXNV], xn[MAXNV], res[MAXNV], dx[MAXNV], Px[MAXNV], Pd[MAXNV],
-        zd[MAXR], gr[MAXNV];
+        zd[MAXR];
     Cmul(s, x, zc);
-    codes_of(s, zc, cd);
+    /* first active-set guess: the ADMM z iterate (the prox output) when there was an ADMM phase,
+       else the rows of C x; later guesses classify C x */
+    codes_of(s, p->method == MPCQP_METHOD_ADMM ? z : zc, cd);
     for (int it = 1; it <= p->polish_max_iter; ++it) {
       pol_it = it;
       for (int r = 0; r < m; ++r) {
@@ -622,32 +614,41 @@ void mpcqp_cpu_solve_one(const mpcqp_params* p, const double* model, double* u0,
         pol_ok = 1;
         break;
       }
-      /* Armijo backtracking on the scaled objective along d = xn - x */
+      /* exact line search along d = xn - x: phi(t) = f(x + t d) is convex piecewise quadratic, its
+         derivative piecewise linear and nondecreasing; semismooth Newton on phi' from t = 1
+         downwards reaches the minimizer in [0, 1] in a few pieces */
       for (int i = 0; i < n; ++i) dx[i] = xn[i] - x[i];
       matvec(n, s->P, x, Px);
       matvec(n, s->P, dx, Pd);
-      for (int r = 0; r < m; ++r) {
-        zd[r] = zn[r] - zc[r];
-        const double rr = zc[r] > s->u[r] ? zc[r] - s->u[r] : (zc[r] < s->l[r] ? zc[r] - s->l[r] : 0.0);
-        tmp[r] = 2.0 * s->w[r] * rr;
-      }
-      CTmul(s, tmp, gr);
-      double slope = 0.0, qd = 0.0, lin = 0.0, q0 = 0.0;
+      for (int r = 0; r < m; ++r) zd[r] = zn[r] - zc[r];
+      double qd = 0.0, lin = 0.0;
       for (int i = 0; i < n; ++i) {
-        slope += (Px[i] + s->q[i] + gr[i]) * dx[i];
         qd += dx[i] * Pd[i];
         lin += (Px[i] + s->q[i]) * dx[i];
-        q0 += x[i] * (0.5 * Px[i] + s->q[i]);
       }
-      const double f0 = q0 + pen(s, zc);
       double t = 1.0;
-      for (int ls = 0; ls < 60; ++ls) {
+      for (int ls = 0; ls < 40; ++ls) {
         ++n_ls;
-        double zt[MAXR];
-        for (int r = 0; r < m; ++r) zt[r] = zc[r] + t * zd[r];
-        const double ft = q0 + t * lin + 0.5 * t * t * qd + pen(s, zt);
-        if (ft <= f0 + 1e-4 * t * slope) break;
-        t *= 0.5;
+        double d1 = lin + t * qd, d2 = qd;
+        for (int r = 0; r < m; ++r) {
+          const double zt = zc[r] + t * zd[r];
+          const double rr = zt > s->u[r] ? zt - s->u[r] : (zt < s->l[r] ? zt - s->l[r] : 0.0);
+          d1 += 2.0 * s->w[r] * rr * zd[r];
+          if (rr != 0.0) d2 += 2.0 * s->w[r] * zd[r] * zd[r];
+        }
+        if (d1 <= 0.0 || !(d2 > 0.0)) break;
+        const double tn = fmax(0.0, t - d1 / d2);
+        if (tn >= t) break;
+        /* same linear piece of phi' at tn as at t: tn is that piece's root, the minimizer */
+        int same = 1;
+        for (int r = 0; r < m && same; ++r) {
+          const double za = zc[r] + t * zd[r], zb = zc[r] + tn * zd[r];
+          const int ca = za > s->u[r] ? 2 : (za < s->l[r] ? 1 : 0);
+          const int cb = zb > s->u[r] ? 2 : (zb < s->l[r] ? 1 : 0);
+          same = ca == cb;
+        }
+        t = tn;
+        if (same) break;
       }
       for (int i = 0; i < n; ++i) x[i] += t * dx[i];
       for (int r = 0; r < m; ++r) zc[r] = zc[r] + t * zd[r];

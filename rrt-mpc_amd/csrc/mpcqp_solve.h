@@ -504,8 +504,8 @@ __device__ __forceinline__ bool setup_qp(const mpcqp_params& p, int b, const dou
 // ------------------------------------------------------------------ K2b: ADMM
 // Returns the ADMM flag (-1 numerical error, 0 not converged, 1 converged); x, it, nfact out.
 template <int N>
-__device__ __forceinline__ int admm_qp(const mpcqp_params& p, Ctx<N>& C, bool bad, double& x_out, int& it_out,
-                                       int& nfact_out, double* __restrict__ dbg) {
+__device__ __forceinline__ int admm_qp(const mpcqp_params& p, Ctx<N>& C, bool bad, double& x_out, double z_out[3],
+                                       int& it_out, int& nfact_out, double* __restrict__ dbg) {
   const bool act = C.act;
   double x = 0.0, z[3] = {0.0, 0.0, 0.0}, y[3] = {0.0, 0.0, 0.0};
   double rho = p.rho;
@@ -636,6 +636,8 @@ __device__ __forceinline__ int admm_qp(const mpcqp_params& p, Ctx<N>& C, bool ba
     }
   }
   x_out = act ? x : 0.0;
+#pragma unroll
+  for (int r = 0; r < 3; ++r) z_out[r] = z[r];
   it_out = it;
   nfact_out = nfact;
   T2.end(0);
@@ -647,7 +649,7 @@ __device__ __forceinline__ int admm_qp(const mpcqp_params& p, Ctx<N>& C, bool ba
 // ------------------------------------------------------------------ K2c: polish + outputs
 template <int N>
 __device__ __forceinline__ void finish_qp(const mpcqp_params& p, int b, const double* __restrict__ model, Ctx<N>& C,
-                                          double x_in, int admm_flag, int admm_it, int nfact,
+                                          double x_in, const double z_admm[3], int admm_flag, int admm_it, int nfact,
                                           double* __restrict__ u0o, double* __restrict__ Xo, double* __restrict__ Uo,
                                           int32_t* __restrict__ statuso, int32_t* __restrict__ iterso,
                                           uint8_t* __restrict__ activeo) {
@@ -669,8 +671,13 @@ __device__ __forceinline__ void finish_qp(const mpcqp_params& p, int b, const do
     double zc[3];
     int cd[3];
     C.Cmul(x, zc);
+    // first active-set guess: the ADMM z iterate (the prox output) after an ADMM phase, else the
+    // rows of C x; later guesses classify C x
 #pragma unroll
-    for (int r = 0; r < 3; ++r) cd[r] = zc[r] > C.hi[r] ? 2 : (zc[r] < C.lo[r] ? 1 : 0);
+    for (int r = 0; r < 3; ++r) {
+      const double zg = use_admm ? z_admm[r] : zc[r];
+      cd[r] = zg > C.hi[r] ? 2 : (zg < C.lo[r] ? 1 : 0);
+    }
     constexpr int kMaxRank1 = n / 2;  // more changed rows than this: refactor (form + sweep)
     double rwf[3] = {0.0, 0.0, 0.0};  // soft-row weights of the current factorization
     bool have_fact = false;
@@ -752,40 +759,45 @@ __device__ __forceinline__ void finish_qp(const mpcqp_params& p, int b, const do
         pol_ok = true;
         break;
       }
-      // Armijo backtracking on the scaled objective along d = xn - x
+      // exact line search along d = xn - x: phi(t) = f(x + t d) is convex piecewise quadratic,
+      // phi' piecewise linear and nondecreasing; semismooth Newton on phi' from t = 1 downwards
+      // lands on the minimizer in [0, 1] after a few pieces (two independent reductions a step)
       T.begin();
       const double dx = act ? xn - x : 0.0;
       const double Px = C.Pmul(x);
       const double Pd = C.Pmul(dx);
-      double zd[3], gt[3];
+      double zd[3];
 #pragma unroll
-      for (int r = 0; r < 3; ++r) {
-        zd[r] = zn[r] - zc[r];
-        const double res = zc[r] > C.hi[r] ? zc[r] - C.hi[r] : (zc[r] < C.lo[r] ? zc[r] - C.lo[r] : 0.0);
-        gt[r] = 2.0 * C.wb[r] * res;
-      }
-      const double gr = C.CTmul(gt);
-      const double slope = wave_sum(act ? (Px + C.qv + gr) * dx : 0.0);
+      for (int r = 0; r < 3; ++r) zd[r] = zn[r] - zc[r];
       const double qd = wave_sum(act ? dx * Pd : 0.0);
       const double lin = wave_sum(act ? (Px + C.qv) * dx : 0.0);
-      const double q0 = wave_sum(act ? x * (0.5 * Px + C.qv) : 0.0);
-      auto pen = [&](double t) -> double {
-        double s = 0.0;
+      double t = 1.0;
+      for (int ls = 0; ls < 40; ++ls) {
+        ++n_ls;
+        double g1 = 0.0, g2 = 0.0;
 #pragma unroll
         for (int r = 0; r < 3; ++r) {
           const double zt = zc[r] + t * zd[r];
-          const double d = zt > C.hi[r] ? zt - C.hi[r] : (zt < C.lo[r] ? C.lo[r] - zt : 0.0);
-          s += C.wb[r] * d * d;
+          const double rr = zt > C.hi[r] ? zt - C.hi[r] : (zt < C.lo[r] ? zt - C.lo[r] : 0.0);
+          g1 += 2.0 * C.wb[r] * rr * zd[r];
+          if (rr != 0.0) g2 += 2.0 * C.wb[r] * zd[r] * zd[r];
         }
-        return wave_sum(s);
-      };
-      const double f0 = q0 + pen(0.0);
-      double t = 1.0;
-      for (int ls = 0; ls < 60; ++ls) {
-        ++n_ls;
-        const double ft = q0 + t * lin + 0.5 * t * t * qd + pen(t);
-        if (ft <= f0 + 1e-4 * t * slope) break;
-        t *= 0.5;
+        const double d1 = lin + t * qd + wave_sum(g1);
+        const double d2 = qd + wave_sum(g2);
+        if (d1 <= 0.0 || !(d2 > 0.0)) break;
+        const double tn = fmax(0.0, t - d1 / d2);
+        if (tn >= t) break;
+        // same linear piece of phi' at tn as at t: tn is that piece's root, the minimizer
+        bool moved = false;
+#pragma unroll
+        for (int r = 0; r < 3; ++r) {
+          const double za = zc[r] + t * zd[r], zb = zc[r] + tn * zd[r];
+          const int ca = za > C.hi[r] ? 2 : (za < C.lo[r] ? 1 : 0);
+          const int cb = zb > C.hi[r] ? 2 : (zb < C.lo[r] ? 1 : 0);
+          moved = moved || ca != cb;
+        }
+        t = tn;
+        if (!wave_any(moved)) break;
       }
       x = x + t * dx;
       C.Cmul(x, zc);
@@ -884,12 +896,15 @@ __global__ __launch_bounds__(kWave) void k_solve(mpcqp_params p, int B, const ui
   const int b = blockIdx.x;
   if (b >= B || (mask && !mask[b])) return;
   double* dbg = p.debug_state ? state + (size_t)b * state_stride(N) : nullptr;
+  const uint64_t t_start = __builtin_amdgcn_s_memtime();
   Ctx<N> C;
   const bool bad = setup_qp<N>(p, b, model, C, sm, state + (size_t)b * state_stride(N), dbg);
-  double x = 0.0;
+  double x = 0.0, z[3] = {0.0, 0.0, 0.0};
   int flag = bad ? -1 : 0, it = 0, nfact = 0;
-  if (p.method == MPCQP_METHOD_ADMM) flag = admm_qp<N>(p, C, bad, x, it, nfact, dbg);
-  finish_qp<N>(p, b, model, C, x, flag, it, nfact, u0o, Xo, Uo, statuso, iterso, activeo);
+  if (p.method == MPCQP_METHOD_ADMM) flag = admm_qp<N>(p, C, bad, x, z, it, nfact, dbg);
+  finish_qp<N>(p, b, model, C, x, z, flag, it, nfact, u0o, Xo, Uo, statuso, iterso, activeo);
+  if (dbg && threadIdx.x == 0)  // this wave's cycles, start to finish (tools/qp_cycles.py)
+    dbg[state_scal_off(N) + 4] = (double)(__builtin_amdgcn_s_memtime() - t_start);
 }
 
 }  // namespace

@@ -42,6 +42,7 @@ def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("config", nargs="?", default="config3")
     ap.add_argument("--worst", type=int, default=-1)
+    ap.add_argument("--by", type=int, default=0, help="iteration counter ranking --worst (0 ADMM, 1 polish)")
     ap.add_argument("--batch", type=int, default=0)
     a = ap.parse_args()
     b = getattr(scenarios, a.config)()
@@ -53,7 +54,7 @@ def main() -> None:
     ctrl.solve_batch(x0, ref, up)
     torch.cuda.synchronize()
     if a.worst >= 0:
-        order = np.argsort(-ctrl._iters[: b.size, 0].cpu().numpy(), kind="stable")
+        order = np.argsort(-ctrl._iters[: b.size, a.by].cpu().numpy(), kind="stable")
         q = int(order[a.worst])
         x0, ref, up = (np.repeat(v[q:q + 1], B, axis=0) for v in (x0, ref, up))
     else:
