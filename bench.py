@@ -69,8 +69,14 @@ def make_batch(config: str, batch_per_gpu: int, world: int, rank: int):
     return b.x0[sl], b.ref[sl], b.u_prev[sl], b.horizon, b.name
 
 
-def cpu_baseline(params, x0, ref, u_prev, seconds: float):
-    """The C restatement (oracle/, kind "port") on the host cores, bounded sample."""
+BASELINE_METRIC = "MPC QP solves/s (horizon=20, batch=4096) @1/2/4/8 GPU; rel-err vs OSQP"
+
+
+def cpu_baseline(params, x0, ref, u_prev, seconds: float, gpu_U=None, gpu_active=None):
+    """The C restatement (oracle/, kind "port") on the host cores, bounded sample.
+
+    As the checker, it also gives the GPU batch's rel-err: the C restatement's polish ends at
+    the exact optimum, which is the OSQP+polish optimum of the reference (a strictly convex QP)."""
     sys.path.insert(0, str(ROOT / "oracle"))
     import cpu_solver
 
@@ -89,7 +95,17 @@ def cpu_baseline(params, x0, ref, u_prev, seconds: float):
         if time.perf_counter() - t0 >= seconds:
             break
     dt = time.perf_counter() - t0
-    return {
+    parity = None
+    if gpu_U is not None:
+        Uc = out["U"]
+        parity = {
+            "vs": "exact optimum (C restatement's polish; = the reference's OSQP+polish optimum)",
+            "qps": int(len(Uc)),
+            "max_rel_err_U": float(np.max(np.abs(gpu_U - Uc).reshape(len(Uc), -1).max(axis=1)
+                                          / np.maximum(1.0, np.abs(Uc).reshape(len(Uc), -1).max(axis=1)))),
+            "active_set_mismatches": int((gpu_active != out["active"]).any(axis=1).sum()),
+        }
+    return parity, {
         "value": solved / dt,
         "unit": "QP/s",
         "cores": threads,
@@ -122,6 +138,9 @@ def main() -> int:
     ap.add_argument("--batch", type=int, default=0, help="QPs per GPU (default: the config's)")
     ap.add_argument("--method", default="admm", choices=["admm", "newton"])
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline sample length (0 = skip)")
+    ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
+                    help="torch.distributed backend for N > 1 (nccl = RCCL; gloo only to rehearse "
+                         "several ranks on one GPU)")
     args = ap.parse_args()
 
     import torch
@@ -130,11 +149,16 @@ def main() -> int:
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    # one process per GPU; ranks beyond the visible devices wrap (rehearsal on one GPU)
+    dev_index = local_rank % max(1, torch.cuda.device_count())
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
-    device = torch.device("cuda", local_rank)
+        torch.cuda.set_device(dev_index)
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", dev_index))
+        else:
+            dist.init_process_group("gloo")
+    device = torch.device("cuda", dev_index)
     torch.cuda.set_device(device)
 
     from mpcqp import _lib
@@ -202,8 +226,10 @@ def main() -> int:
         achieved_tf = float(flops.sum()) / (k2_ms * 1e-3) / 1e12  # rank-0 K2 launch, algorithmic flops
         hbm_gbs = B * qp_bytes(N) / (ms_per_step * 1e-3) / 1e9
         traffic = load_pmc_traffic(N, B)
+        metric = BASELINE_METRIC if (args.config, N, B) == ("config3", 20, 4096) else \
+            f"MPC QP solves/s (horizon={N}, batch={B} per GPU)"
         out = {
-            "metric": f"MPC QP solves/s (horizon={N}, batch={B} per GPU)",
+            "metric": metric,
             "value": value,
             "unit": "QP/s",
             "n_gpus": world,
@@ -253,7 +279,8 @@ def main() -> int:
             },
         }
         if world == 1 and args.cpu_seconds > 0:
-            out["cpu_baseline"] = cpu_baseline(params, x0, ref, u_prev, args.cpu_seconds)
+            out["rel_err"], out["cpu_baseline"] = cpu_baseline(
+                params, x0, ref, u_prev, args.cpu_seconds, ctrl._U[:B].cpu().numpy(), ctrl._active[:B].cpu().numpy())
         print(json.dumps(out), flush=True)
     ctrl.close()
     if world > 1:
