@@ -115,13 +115,13 @@ struct Ctx {
     const double Dm = ln < n ? D : 0.0;
     double wD[4];
     bcast<kNW>(Dm, wD);  // D_j of every lane j
+    // v-row weight sums sv[max(lane, j) / 2]: the lane's own entry for j <= lane (one read),
+    // a wave-uniform entry for j > lane
+    const double sv_own = ev_ln ? sv[ln >> 1] : 0.0;
     Unroll<0, n>::run([&](auto jc) {
       constexpr int j = decltype(jc)::value;
       double t = 0.0;
-      if ((j & 1) == 0 && ev_ln) {
-        const int mx = (ln > j ? ln : j) >> 1;
-        t = dt * dt * sv[mx];
-      }
+      if ((j & 1) == 0 && ev_ln) t = dt * dt * (ln > j ? sv_own : sv[j >> 1]);
       if (j == ln) t += diag;
       if (j == ln + 2) t -= du2n;
       if (j + 2 == ln) t -= du2;
