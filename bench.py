@@ -72,6 +72,16 @@ def make_batch(config: str, batch_per_gpu: int, world: int, rank: int):
 BASELINE_METRIC = "MPC QP solves/s (horizon=20, batch=4096) @1/2/4/8 GPU; rel-err vs OSQP"
 
 
+def _cpu_model() -> str:
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return platform.processor() or platform.machine()
+
+
 def cpu_baseline(params, x0, ref, u_prev, seconds: float, gpu_U=None, gpu_active=None):
     """The C restatement (oracle/, kind "port") on the host cores, bounded sample.
 
@@ -95,6 +105,12 @@ def cpu_baseline(params, x0, ref, u_prev, seconds: float, gpu_U=None, gpu_active
         if time.perf_counter() - t0 >= seconds:
             break
     dt = time.perf_counter() - t0
+    # the 1-core figure SURVEY.md 8(d) asks for beside the all-core one (a short slice)
+    n1, t1 = 0, time.perf_counter()
+    while time.perf_counter() - t1 < min(3.0, seconds / 3):
+        out1 = cpu_solver.cpu_solve(params, x0[:256], ref[:256], u_prev[:256], nthreads=1)
+        n1 += int((out1["status"] == 1).sum())
+    dt1 = time.perf_counter() - t1
     parity = None
     if gpu_U is not None:
         Uc = out["U"]
@@ -110,6 +126,8 @@ def cpu_baseline(params, x0, ref, u_prev, seconds: float, gpu_U=None, gpu_active
         "unit": "QP/s",
         "cores": threads,
         "kind": "port",
+        "value_1core": n1 / dt1,
+        "cpu_model": _cpu_model(),
         "sample": f"{done} QPs ({done // len(x0)} passes over this rank's batch) in {dt:.1f} s, "
                   f"C restatement of the same ADMM+polish algorithm (oracle/mpcqp_cpu.c, OpenMP), "
                   f"host {platform.processor() or platform.machine()}",
@@ -117,14 +135,13 @@ def cpu_baseline(params, x0, ref, u_prev, seconds: float, gpu_U=None, gpu_active
 
 
 def load_pmc_traffic(N: int, batch: int):
-    """HBM bytes per K2 launch from the committed rocprofv3 PMC summary, if present."""
+    """This workload's entry of the committed rocprofv3 PMC summary (HBM bytes, SQ counters), if present."""
     p = ROOT / "profiles" / "pmc_traffic.json"
     if not p.exists():
         return None
     try:
         d = json.loads(p.read_text())
-        key = f"N{N}_B{batch}"
-        return d.get(key, {}).get("k_solve_hbm_bytes_per_launch")
+        return d.get(f"N{N}_B{batch}") or None
     except Exception:
         return None
 
@@ -225,7 +242,9 @@ def main() -> int:
         ms_per_step = 1000.0 * T / args.steps
         achieved_tf = float(flops.sum()) / (k2_ms * 1e-3) / 1e12  # rank-0 K2 launch, algorithmic flops
         hbm_gbs = B * qp_bytes(N) / (ms_per_step * 1e-3) / 1e9
-        traffic = load_pmc_traffic(N, B)
+        pmc = load_pmc_traffic(N, B) or {}
+        traffic = pmc.get("k_solve_hbm_bytes_per_launch")
+        hw_flops = (pmc.get("k_solve_sq") or {}).get("hw_fp64_flops_per_launch")
         metric = BASELINE_METRIC if (args.config, N, B) == ("config3", 20, 4096) else \
             f"MPC QP solves/s (horizon={N}, batch={B} per GPU)"
         out = {
@@ -265,6 +284,9 @@ def main() -> int:
                 "frac": achieved_tf / FP64_PEAK_TFLOPS,
                 "traffic": traffic,
                 "kernel": "k_solve",
+                # the hardware's own count (SQ_INSTS_VALU_FLOPS_FP64, committed PMC pass) over this launch time
+                "hw_flops_per_launch": hw_flops,
+                "hw_frac": hw_flops / (k2_ms * 1e-3) / 1e12 / FP64_PEAK_TFLOPS if hw_flops else None,
                 "note": "FP64 compute roof (MI355X FP64 vector peak == FP64 matrix peak); k_solve is a "
                         "latency-bound FP64 VALU kernel. Flops = bench.qp_flops (as implemented, counted "
                         "per QP from the kernel's iteration counters) / mean k_solve event time.",

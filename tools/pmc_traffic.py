@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Fold rocprofv3 --pmc passes (FETCH_SIZE, WRITE_SIZE, TCC_EA0_*REQ) into profiles/pmc_traffic.json.
+"""Fold rocprofv3 --pmc passes (FETCH_SIZE, WRITE_SIZE, TCC_EA0_*REQ, SQ_*) into profiles/pmc_traffic.json.
 
     python tools/pmc_traffic.py gpurun_out --N 20 --B 4096 > profiles/pmc_traffic.json
 
@@ -41,7 +41,7 @@ def main() -> None:
     a = ap.parse_args()
     d = Path(a.out_dir)
     c = {}
-    for p in ("pmc_fetch", "pmc_write", "pmc_req"):
+    for p in ("pmc_fetch", "pmc_write", "pmc_req", "pmc_sq", "pmc_f64"):
         f = d / p / "run_counter_collection.csv"
         if f.exists():
             c.update(per_kernel(f))
@@ -70,6 +70,23 @@ def main() -> None:
                     "writes the outputs; the scaled problem stays on chip",
         }
     }
+    sq = {name: v for (k, name), v in c.items() if k == "k_solve" and name.startswith("SQ_")}
+    if sq:
+        # SQ_WAVE_CYCLES / WAIT_* / ACTIVE_INST_* count quad-cycles (MI355X_MICROARCH.md constants)
+        cyc = sq.get("SQ_WAVE_CYCLES")
+        out[f"N{N}_B{B}"]["k_solve_sq"] = {
+            "counters_per_launch": sq,
+            # SQ_INSTS_VALU_FLOPS_FP64 counts per wave instruction (FMA 2, ADD/MUL/TRANS 1: it equals
+            # 2*FMA+ADD+MUL+TRANS below); x64 lanes = executed flops, masked lanes included
+            "hw_fp64_flops_per_launch": 64.0 * sq["SQ_INSTS_VALU_FLOPS_FP64"] if "SQ_INSTS_VALU_FLOPS_FP64" in sq else None,
+            "wave_cycles_per_wave": 4.0 * cyc / sq["SQ_WAVES"] if cyc and sq.get("SQ_WAVES") else None,
+            "frac_wait_any": sq["SQ_WAIT_ANY"] / cyc if cyc and "SQ_WAIT_ANY" in sq else None,
+            "frac_wait_inst_any": sq["SQ_WAIT_INST_ANY"] / cyc if cyc and "SQ_WAIT_INST_ANY" in sq else None,
+            "frac_active_inst_any": sq["SQ_ACTIVE_INST_ANY"] / cyc if cyc and "SQ_ACTIVE_INST_ANY" in sq else None,
+            "f64_valu_insts_per_wave": (sum(sq.get(f"SQ_INSTS_VALU_{o}_F64", 0.0) for o in ("FMA", "ADD", "MUL", "TRANS"))
+                                        / sq["SQ_WAVES"]) if sq.get("SQ_WAVES") else None,
+            "valu_insts_per_wave": sq["SQ_INSTS_VALU"] / sq["SQ_WAVES"] if sq.get("SQ_WAVES") and "SQ_INSTS_VALU" in sq else None,
+        }
     print(json.dumps(out, indent=1))
 
 
