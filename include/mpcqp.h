@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define MPCQP_ABI_VERSION 1
+#define MPCQP_ABI_VERSION 2
 
 /* error codes (function return values) */
 #define MPCQP_OK 0
@@ -95,6 +95,11 @@ typedef struct mpcqp_params {
   int32_t polish;             /* 1 */
   int32_t polish_max_iter;    /* 100 */
   int32_t debug_state;        /* 1: also write the per-QP solver state buffer (mpcqp_state_buffer; tests) */
+  int32_t polish_from;        /* 150: from this ADMM iteration on, every termination check also tries the
+                                 polish (capped at polish_attempt_max_iter); a polish that reaches a
+                                 self-consistent active set is the exact optimum and ends the solve as
+                                 solved, a failed attempt resumes ADMM.  0: polish only after ADMM stops */
+  int32_t polish_attempt_max_iter; /* 30 */
 } mpcqp_params;
 
 typedef struct mpcqp_ws mpcqp_ws;

@@ -10,13 +10,18 @@
  *             linearize() at ref[max(k-1,0)], u = 0       mpc_controller.py:65-70,108
  *                                                         vehicle_model.py:24-45
  *   condense: states and slacks eliminated; the QP of      mpc_controller.py:53-117
- *             mpc_controller.py becomes min U'HU+2g'U+sum w dist(CU+b,[lo,hi])^2
+ *             mpc_controller.py becomes min W'HW+2g'W+sum w dist(CW+b,[lo,hi])^2 over
+ *             W = (v_1, delta_0, v_2, delta_1, ...): the speeds replace the accelerations
+ *             (a_k = (v_{k+1} - v_k)/dt, a bijective affine change of variables, same
+ *             optimum), so every constraint row is banded: v rows identity, a rows first
+ *             differences, da rows second differences
  *   solve   : OSQP's algorithm with the reference settings (mpc_controller.py:121-131):
  *             Ruiz scaling (10 it) + cost scaling, ADMM (rho 0.1, sigma 1e-6,
  *             alpha 1.6), adaptive rho, eps_abs = eps_rel = 1e-3 termination;
  *             the projection onto [l,u] is the prox of w*dist^2 (slacks eliminated);
  *             then polish = semismooth-Newton active-set iteration until the
- *             active set reproduces itself (exact optimum).
+ *             active set reproduces itself (exact optimum).  From ADMM iteration
+ *             polish_from on, each termination check also attempts the polish.
  *
  * Parity of this file's *solutions* is pinned against oracle/mpc_oracle.py's exact
  * solve (tests/test_oracle.py); it is the reference implementation for the GPU's
@@ -116,6 +121,10 @@ typedef struct {
   double q[MAXNV];
   double D[MAXNV], E[MAXR], c;
   double l[MAXR], u[MAXR], w[MAXR]; /* scaled bounds and prox weights */
+  /* unscaled row coefficients on the lane's own variable and the same-kind variables 1 and 2
+     steps back: a row (input p) = k1[p][0] W_p + k1[p][1] W_{p-2}, rate row p =
+     k2[p][0] W_p + k2[p][1] W_{p-2} + k2[p][2] W_{p-4}; v row j = W_{2j} */
+  double k1[MAXNV][2], k2[MAXNV][3];
   double dt;
   double K[MAXNV][MAXNV]; /* inverse workspace */
   double M[MAXNV][MAXNV];
@@ -127,62 +136,61 @@ static inline double limit_scaling(double v) {
   return v;
 }
 
-/* z = Cbar x  (structured: v rows prefix sums, u rows identity, du rows differences) */
+/* z = Cbar x  (banded: v rows identity, input rows first, rate rows second differences) */
 static void Cmul(const qp_t* s, const double* x, double* z) {
   const int N = s->N, n = s->n;
-  double acc = 0.0;
-  for (int j = 0; j < N; ++j) {
-    acc += s->D[2 * j] * x[2 * j];
-    z[j] = s->E[j] * s->dt * acc; /* v row j+1 */
-  }
+  double t[MAXNV + 4];
+  t[0] = t[1] = t[2] = t[3] = 0.0; /* t[p + 4] = D_p x_p */
+  for (int p = 0; p < n; ++p) t[p + 4] = s->D[p] * x[p];
+  for (int j = 0; j < N; ++j) z[j] = s->E[j] * t[2 * j + 4];
   for (int p = 0; p < n; ++p) {
-    z[N + p] = s->E[N + p] * (s->D[p] * x[p]);
-    double d = s->D[p] * x[p];
-    if (p >= 2) d -= s->D[p - 2] * x[p - 2];
-    z[3 * N + p] = s->E[3 * N + p] * d;
+    const double e1 = s->E[N + p], e2 = s->E[3 * N + p];
+    z[N + p] = (e1 * s->k1[p][0]) * t[p + 4] + (e1 * s->k1[p][1]) * t[p + 2];
+    z[3 * N + p] = ((e2 * s->k2[p][0]) * t[p + 4] + (e2 * s->k2[p][1]) * t[p + 2]) + (e2 * s->k2[p][2]) * t[p];
   }
 }
 
 /* x = Cbar' y */
 static void CTmul(const qp_t* s, const double* y, double* x) {
   const int N = s->N, n = s->n;
-  double suf = 0.0;
-  for (int j = N - 1; j >= 0; --j) {
-    suf += s->E[j] * y[j];
-    x[2 * j] = s->dt * suf;
-    x[2 * j + 1] = 0.0;
+  double a1[MAXNV + 4], a2[MAXNV + 4], b2[MAXNV + 4]; /* per row: terms for the variable 2 / 4 back */
+  for (int p = 0; p < n + 4; ++p) a1[p] = a2[p] = b2[p] = 0.0;
+  for (int p = 0; p < n; ++p) {
+    const double e1 = s->E[N + p], e2 = s->E[3 * N + p];
+    a1[p] = (e1 * s->k1[p][1]) * y[N + p] + (e2 * s->k2[p][1]) * y[3 * N + p];
+    b2[p] = (e2 * s->k2[p][2]) * y[3 * N + p];
   }
   for (int p = 0; p < n; ++p) {
-    double t = x[p] + s->E[N + p] * y[N + p] + s->E[3 * N + p] * y[3 * N + p];
-    if (p + 2 < n) t -= s->E[3 * N + p + 2] * y[3 * N + p + 2];
+    const double e1 = s->E[N + p], e2 = s->E[3 * N + p];
+    double t = ((p & 1) == 0 ? s->E[p / 2] * y[p / 2] : 0.0) + (e1 * s->k1[p][0]) * y[N + p];
+    t += (e2 * s->k2[p][0]) * y[3 * N + p];
+    t += a1[p + 2];
+    t += b2[p + 4];
     x[p] = s->D[p] * t;
   }
+  (void)a2;
 }
 
-/* A = Pbar + sig I + Cbar' diag(rw) Cbar  (rw per ADMM row) */
+/* A = Pbar + sig I + Cbar' diag(rw) Cbar  (rw per ADMM row); the row part is banded */
 static void form_kkt(const qp_t* s, double sig, const double* rw, double A[MAXNV][MAXNV]) {
   const int N = s->N, n = s->n;
-  double Sv[MAXN + 2];
-  Sv[N] = 0.0;
-  for (int j = N - 1; j >= 0; --j) Sv[j] = Sv[j + 1] + s->E[j] * s->E[j] * rw[j]; /* sum over v rows k>=j+1 */
-  for (int i = 0; i < n; ++i) {
-    for (int j = 0; j < n; ++j) {
-      double t = 0.0;
-      if ((i & 1) == 0 && (j & 1) == 0) {
-        int mx = (i > j ? i : j) / 2;
-        t = s->dt * s->dt * Sv[mx];
-      }
-      if (i == j) {
-        t += s->E[N + i] * s->E[N + i] * rw[N + i] + s->E[3 * N + i] * s->E[3 * N + i] * rw[3 * N + i];
-        if (i + 2 < n) t += s->E[3 * N + i + 2] * s->E[3 * N + i + 2] * rw[3 * N + i + 2];
-      } else if (j == i + 2) {
-        t -= s->E[3 * N + j] * s->E[3 * N + j] * rw[3 * N + j];
-      } else if (i == j + 2) {
-        t -= s->E[3 * N + i] * s->E[3 * N + i] * rw[3 * N + i];
-      }
-      A[i][j] = s->P[i][j] + s->D[i] * s->D[j] * t + (i == j ? sig : 0.0);
-    }
+  static _Thread_local double Bd[MAXNV][MAXNV];
+  for (int i = 0; i < n; ++i)
+    for (int j = 0; j < n; ++j) Bd[i][j] = 0.0;
+  for (int j = 0; j < N; ++j) Bd[2 * j][2 * j] += s->E[j] * s->E[j] * rw[j];
+  for (int p = 0; p < n; ++p) {
+    const double e1 = s->E[N + p], e2 = s->E[3 * N + p];
+    const double c1[2] = {e1 * s->k1[p][0], e1 * s->k1[p][1]};
+    const double c2[3] = {e2 * s->k2[p][0], e2 * s->k2[p][1], e2 * s->k2[p][2]};
+    for (int a = 0; a < 2; ++a)
+      for (int b = 0; b < 2; ++b)
+        if (c1[a] != 0.0 && c1[b] != 0.0) Bd[p - 2 * a][p - 2 * b] += rw[N + p] * c1[a] * c1[b];
+    for (int a = 0; a < 3; ++a)
+      for (int b = 0; b < 3; ++b)
+        if (c2[a] != 0.0 && c2[b] != 0.0) Bd[p - 2 * a][p - 2 * b] += rw[3 * N + p] * c2[a] * c2[b];
   }
+  for (int i = 0; i < n; ++i)
+    for (int j = 0; j < n; ++j) A[i][j] = s->P[i][j] + s->D[i] * s->D[j] * Bd[i][j] + (i == j ? sig : 0.0);
 }
 
 /* in-place symmetric sweep: A <- A^{-1} (SPD, no pivoting).  returns 0 / -1 on bad pivot */
@@ -225,7 +233,9 @@ static double vmaxabs(int n, const double* x) {
   return m;
 }
 
-/* condensed H, g from the LTV model (backward adjoint recursion per column) */
+/* condensed H, g over W = (v_1, delta_0, v_2, delta_1, ...) from the LTV model (backward
+   adjoint recursion per column).  x_{k+1} = x_k + al_k psi_k + be_k v_k + c0_k (y likewise
+   with ga, et, c1), psi_{k+1} = psi_k + si_k delta_k, v_k = W_{2k-2} (k >= 1), v_0 = x0[3]. */
 static void condense(const mpcqp_params* p, const double* model, qp_t* s) {
   const int N = p->horizon, n = 2 * N;
   const double* al = model;
@@ -246,32 +256,31 @@ static void condense(const mpcqp_params* p, const double* model, qp_t* s) {
     }
   for (int i = 0; i < 2; ++i)
     for (int j = 0; j < 2; ++j) R[i][j] = 0.5 * (p->r[2 * i + j] + p->r[2 * j + i]);
-  double Pa[MAXN + 1], Pb[MAXN + 1], Pg[MAXN + 1], Pe[MAXN + 1];
-  Pa[0] = Pb[0] = Pg[0] = Pe[0] = 0.0;
+  double Pa[MAXN + 1], Pg[MAXN + 1];
+  Pa[0] = Pg[0] = 0.0;
   for (int k = 0; k < N; ++k) {
     Pa[k + 1] = Pa[k] + al[k];
-    Pb[k + 1] = Pb[k] + be[k];
     Pg[k + 1] = Pg[k] + ga[k];
-    Pe[k + 1] = Pe[k] + et[k];
   }
-  /* free response error e_m = sx_m - r_m */
+  /* free response (W = 0: v_k = 0 for k >= 1, constant heading) error e_m = sx_m - r_m */
   double e[MAXN + 1][4];
   {
     double px = x0[0], py = x0[1];
-    const double psi = x0[2], v = x0[3];
+    const double psi = x0[2];
     for (int m = 1; m <= N; ++m) {
       const int k = m - 1;
+      const double v = k == 0 ? x0[3] : 0.0;
       px = px + al[k] * psi + be[k] * v + c0[k];
       py = py + ga[k] * psi + et[k] * v + c1[k];
       e[m][0] = px - r[4 * m + 0];
       e[m][1] = py - r[4 * m + 1];
       e[m][2] = psi - r[4 * m + 2];
-      e[m][3] = v - r[4 * m + 3];
+      e[m][3] = 0.0 - r[4 * m + 3];
     }
   }
   for (int col = 0; col <= n; ++col) {
     const int j = col >> 1, c = col & 1;
-    double mu[4] = {0, 0, 0, 0};
+    double mu[3] = {0, 0, 0};
     for (int m = N; m >= 1; --m) {
       double sv[4];
       if (col == n) {
@@ -279,48 +288,61 @@ static void condense(const mpcqp_params* p, const double* model, qp_t* s) {
         sv[1] = e[m][1];
         sv[2] = e[m][2];
         sv[3] = e[m][3];
-      } else if (m > j) {
-        if (c == 0) {
-          sv[0] = dt * (Pb[m] - Pb[j + 1]);
-          sv[1] = dt * (Pe[m] - Pe[j + 1]);
-          sv[2] = 0.0;
-          sv[3] = dt;
-        } else {
-          sv[0] = si[j] * (Pa[m] - Pa[j + 1]);
-          sv[1] = si[j] * (Pg[m] - Pg[j + 1]);
-          sv[2] = si[j];
-          sv[3] = 0.0;
-        }
+      } else if (c == 0) { /* v_{j+1}: itself at m = j+1, positions from m = j+2 on */
+        const int on = m >= j + 2;
+        sv[0] = on ? be[j + 1] : 0.0;
+        sv[1] = on ? et[j + 1] : 0.0;
+        sv[2] = 0.0;
+        sv[3] = m == j + 1 ? 1.0 : 0.0;
+      } else if (m > j) { /* delta_j */
+        sv[0] = si[j] * (Pa[m] - Pa[j + 1]);
+        sv[1] = si[j] * (Pg[m] - Pg[j + 1]);
+        sv[2] = si[j];
+        sv[3] = 0.0;
       } else {
         sv[0] = sv[1] = sv[2] = sv[3] = 0.0;
       }
       double (*W)[4] = (m == N) ? QN : Q;
       double ws[4];
       for (int a = 0; a < 4; ++a) ws[a] = W[a][0] * sv[0] + W[a][1] * sv[1] + W[a][2] * sv[2] + W[a][3] * sv[3];
+      /* row v_m: own cost term + the positions after it; row delta_{m-1}: si * heading adjoint */
+      double hv;
       if (m < N) {
         const double m0 = mu[0], m1 = mu[1];
+        hv = ws[3] + (be[m] * m0 + et[m] * m1);
         mu[0] = ws[0] + m0;
         mu[1] = ws[1] + m1;
         mu[2] = ws[2] + (mu[2] + al[m] * m0 + ga[m] * m1);
-        mu[3] = ws[3] + (mu[3] + be[m] * m0 + et[m] * m1);
       } else {
+        hv = ws[3];
         mu[0] = ws[0];
         mu[1] = ws[1];
         mu[2] = ws[2];
-        mu[3] = ws[3];
       }
-      const double ha = dt * mu[3], hd = si[m - 1] * mu[2];
+      const double hd = si[m - 1] * mu[2];
       if (col == n) {
-        s->g[2 * (m - 1)] = ha;
+        s->g[2 * (m - 1)] = hv;
         s->g[2 * (m - 1) + 1] = hd;
       } else {
-        s->H[2 * (m - 1)][col] = ha;
+        s->H[2 * (m - 1)][col] = hv;
         s->H[2 * (m - 1) + 1][col] = hd;
       }
     }
-    if (col < n) {
-      s->H[2 * j][col] += R[0][c];
-      s->H[2 * j + 1][col] += R[1][c];
+    /* input cost sum_k U_k' R U_k with a_k = (v_{k+1} - v_k)/dt: banded in W */
+    const double r00 = R[0][0] / (dt * dt), r10 = R[1][0] / dt;
+    if (col == n) { /* the v_0 = x0[3] end of a_0 */
+      s->g[0] += -x0[3] * r00;
+      s->g[1] += -x0[3] * r10;
+    } else if (c == 0) {
+      s->H[col][col] += j + 1 < N ? 2.0 * r00 : r00;
+      if (j >= 1) s->H[col - 2][col] += -r00;
+      if (j + 1 < N) s->H[col + 2][col] += -r00;
+      s->H[col + 1][col] += r10;
+      if (j + 1 < N) s->H[col + 3][col] += -r10;
+    } else {
+      s->H[col - 1][col] += r10;
+      if (j >= 1) s->H[col - 3][col] += -r10;
+      s->H[col][col] += R[1][1];
     }
   }
 }
@@ -345,50 +367,69 @@ static void setup_qp(const mpcqp_params* p, const double* model, qp_t* s) {
     s->q[i] = 2.0 * s->g[i];
     for (int j = 0; j < n; ++j) s->P[i][j] = 2.0 * s->H[i][j];
   }
+  const double dt = p->dt, idt = 1.0 / p->dt, v0 = x0[3];
+  for (int q = 0; q < n; ++q) {
+    if ((q & 1) == 0) {
+      s->k1[q][0] = idt;
+      s->k1[q][1] = q >= 2 ? -idt : 0.0;
+      s->k2[q][0] = idt;
+      s->k2[q][1] = q >= 2 ? -2.0 * idt : 0.0;
+      s->k2[q][2] = q >= 4 ? idt : 0.0;
+    } else {
+      s->k1[q][0] = 1.0;
+      s->k1[q][1] = 0.0;
+      s->k2[q][0] = 1.0;
+      s->k2[q][1] = q >= 3 ? -1.0 : 0.0;
+      s->k2[q][2] = 0.0;
+    }
+  }
+  (void)dt;
+  /* bounds with the rows' constant parts (v_0 = x0[3], u_prev) moved across */
   double lo0[MAXR], hi0[MAXR], w0[MAXR];
   for (int j = 0; j < N; ++j) {
-    lo0[j] = p->v_bounds[0] - x0[3];
-    hi0[j] = p->v_bounds[1] - x0[3];
+    lo0[j] = p->v_bounds[0];
+    hi0[j] = p->v_bounds[1];
     w0[j] = p->slack_velocity;
   }
   for (int q = 0; q < n; ++q) {
     const int c = q & 1;
-    lo0[N + q] = p->u_bounds[2 * c];
-    hi0[N + q] = p->u_bounds[2 * c + 1];
+    const double ofa = q == 0 ? v0 * idt : 0.0;                                    /* a_0 = (v_1 - v_0)/dt */
+    const double ofr = q < 2 ? up[c] + ofa : (q == 2 ? -v0 * idt : 0.0);          /* a_1 - a_0 carries +v_0/dt */
+    lo0[N + q] = p->u_bounds[2 * c] + ofa;
+    hi0[N + q] = p->u_bounds[2 * c + 1] + ofa;
     w0[N + q] = p->slack_input;
-    const double off = q < 2 ? up[c] : 0.0; /* du row k=0: U - u_prev */
-    lo0[3 * N + q] = p->du_bounds[2 * c] + off;
-    hi0[3 * N + q] = p->du_bounds[2 * c + 1] + off;
+    lo0[3 * N + q] = p->du_bounds[2 * c] + ofr;
+    hi0[3 * N + q] = p->du_bounds[2 * c + 1] + ofr;
     w0[3 * N + q] = p->slack_rate;
   }
-  /* ---- Ruiz equilibration (OSQP scale_data) ---- */
+  /* ---- Ruiz equilibration (OSQP scale_data) on the KKT columns / constraint rows ---- */
   for (int i = 0; i < n; ++i) s->D[i] = 1.0;
   for (int r = 0; r < m; ++r) s->E[r] = 1.0;
   s->c = 1.0;
   for (int it = 0; it < p->scaling; ++it) {
     double dl[MAXNV], el[MAXR];
-    double sufE[MAXN + 1];
-    sufE[N] = 0.0;
-    for (int j = N - 1; j >= 0; --j) sufE[j] = fmax(sufE[j + 1], s->E[j]);
     for (int q = 0; q < n; ++q) {
       double cp = 0.0;
       for (int i = 0; i < n; ++i) cp = fmax(cp, fabs(s->P[i][q]));
-      double cc = fmax(s->E[N + q], s->E[3 * N + q]);
-      if (q + 2 < n) cc = fmax(cc, s->E[3 * N + q + 2]);
-      if ((q & 1) == 0) cc = fmax(cc, s->dt * sufE[q / 2]);
+      /* column q of Cbar: its own v / input / rate rows, the rows 2 and 4 ahead */
+      double cc = (q & 1) == 0 ? s->E[q / 2] : 0.0;
+      cc = fmax(cc, s->E[N + q] * fabs(s->k1[q][0]));
+      cc = fmax(cc, s->E[3 * N + q] * fabs(s->k2[q][0]));
+      if (q + 2 < n) {
+        cc = fmax(cc, s->E[N + q + 2] * fabs(s->k1[q + 2][1]));
+        cc = fmax(cc, s->E[3 * N + q + 2] * fabs(s->k2[q + 2][1]));
+      }
+      if (q + 4 < n) cc = fmax(cc, s->E[3 * N + q + 4] * fabs(s->k2[q + 4][2]));
       cc *= s->D[q];
       dl[q] = 1.0 / sqrt(limit_scaling(fmax(cp, cc)));
     }
-    double pre = 0.0;
-    for (int j = 0; j < N; ++j) {
-      pre = fmax(pre, s->D[2 * j]);
-      el[j] = 1.0 / sqrt(limit_scaling(s->E[j] * s->dt * pre));
-    }
+    for (int j = 0; j < N; ++j) el[j] = 1.0 / sqrt(limit_scaling(s->E[j] * s->D[2 * j]));
     for (int q = 0; q < n; ++q) {
-      el[N + q] = 1.0 / sqrt(limit_scaling(s->E[N + q] * s->D[q]));
-      double dm = s->D[q];
-      if (q >= 2) dm = fmax(dm, s->D[q - 2]);
-      el[3 * N + q] = 1.0 / sqrt(limit_scaling(s->E[3 * N + q] * dm));
+      const double dm2 = q >= 2 ? s->D[q - 2] : 0.0, dm4 = q >= 4 ? s->D[q - 4] : 0.0;
+      const double r1 = fmax(fabs(s->k1[q][0]) * s->D[q], fabs(s->k1[q][1]) * dm2);
+      const double r2 = fmax(fmax(fabs(s->k2[q][0]) * s->D[q], fabs(s->k2[q][1]) * dm2), fabs(s->k2[q][2]) * dm4);
+      el[N + q] = 1.0 / sqrt(limit_scaling(s->E[N + q] * r1));
+      el[3 * N + q] = 1.0 / sqrt(limit_scaling(s->E[3 * N + q] * r2));
     }
     for (int i = 0; i < n; ++i) {
       s->D[i] *= dl[i];
@@ -445,6 +486,89 @@ void mpcqp_cpu_state(const mpcqp_params* p, const double* model, double* out) {
   out[lane_off + 15 * 64] = s->c;
 }
 
+/* ---------------------------------------------------------------- polish */
+/* Semismooth Newton / active-set iteration on the scaled problem from x (in/out): the first
+   active-set guess classifies zg, later ones C x.  Each pass solves the Newton system of the
+   current set (with one step of iterative refinement); a set that reproduces itself is the
+   exact optimum (returns 1, x = that optimum); otherwise an exact line search along the Newton
+   step.  0: not found within max_it passes (x = the last iterate), -1: numerical failure. */
+static int polish_run(qp_t* s, double* x, const double* zg, int max_it, int* pol_it, int* n_fact, int* n_ls) {
+  const int n = s->n, m = s->m;
+  uint8_t cd[MAXR], cn[MAXR];
+  double zc[MAXR], rw[MAXR], tmp[MAXR], rhs[MAXNV], xn[MAXNV], res[MAXNV], dx[MAXNV], Px[MAXNV], Pd[MAXNV], zd[MAXR],
+      zn[MAXR];
+  Cmul(s, x, zc);
+  codes_of(s, zg, cd);
+  for (int it = 1; it <= max_it; ++it) {
+    ++*pol_it;
+    for (int r = 0; r < m; ++r) {
+      rw[r] = cd[r] ? 2.0 * s->w[r] : 0.0;
+      tmp[r] = cd[r] == 2 ? rw[r] * s->u[r] : (cd[r] == 1 ? rw[r] * s->l[r] : 0.0);
+    }
+    form_kkt(s, 0.0, rw, s->M);
+    ++*n_fact;
+    memcpy(s->K, s->M, sizeof(s->M));
+    if (sweep_inverse(n, s->K)) return -1;
+    CTmul(s, tmp, rhs);
+    for (int i = 0; i < n; ++i) rhs[i] -= s->q[i];
+    matvec(n, s->K, rhs, xn);
+    /* one step of iterative refinement */
+    matvec(n, s->M, xn, res);
+    for (int i = 0; i < n; ++i) res[i] = rhs[i] - res[i];
+    matvec(n, s->K, res, dx);
+    for (int i = 0; i < n; ++i) xn[i] += dx[i];
+    Cmul(s, xn, zn);
+    codes_of(s, zn, cn);
+    int nonfinite = 0;
+    for (int i = 0; i < n; ++i) nonfinite |= !isfinite(xn[i]);
+    if (nonfinite) return -1;
+    if (memcmp(cn, cd, m) == 0) {
+      memcpy(x, xn, sizeof(double) * n);
+      return 1;
+    }
+    /* exact line search along d = xn - x: phi(t) = f(x + t d) is convex piecewise quadratic, its
+       derivative piecewise linear and nondecreasing; semismooth Newton on phi' from t = 1
+       downwards reaches the minimizer in [0, 1] in a few pieces */
+    for (int i = 0; i < n; ++i) dx[i] = xn[i] - x[i];
+    matvec(n, s->P, x, Px);
+    matvec(n, s->P, dx, Pd);
+    for (int r = 0; r < m; ++r) zd[r] = zn[r] - zc[r];
+    double qd = 0.0, lin = 0.0;
+    for (int i = 0; i < n; ++i) {
+      qd += dx[i] * Pd[i];
+      lin += (Px[i] + s->q[i]) * dx[i];
+    }
+    double t = 1.0;
+    for (int ls = 0; ls < 40; ++ls) {
+      ++*n_ls;
+      double d1 = lin + t * qd, d2 = qd;
+      for (int r = 0; r < m; ++r) {
+        const double zt = zc[r] + t * zd[r];
+        const double rr = zt > s->u[r] ? zt - s->u[r] : (zt < s->l[r] ? zt - s->l[r] : 0.0);
+        d1 += 2.0 * s->w[r] * rr * zd[r];
+        if (rr != 0.0) d2 += 2.0 * s->w[r] * zd[r] * zd[r];
+      }
+      if (d1 <= 0.0 || !(d2 > 0.0)) break;
+      const double tn = fmax(0.0, t - d1 / d2);
+      if (tn >= t) break;
+      /* same linear piece of phi' at tn as at t: tn is that piece's root, the minimizer */
+      int same = 1;
+      for (int r = 0; r < m && same; ++r) {
+        const double za = zc[r] + t * zd[r], zb = zc[r] + tn * zd[r];
+        const int ca = za > s->u[r] ? 2 : (za < s->l[r] ? 1 : 0);
+        const int cb = zb > s->u[r] ? 2 : (zb < s->l[r] ? 1 : 0);
+        same = ca == cb;
+      }
+      t = tn;
+      if (same) break;
+    }
+    for (int i = 0; i < n; ++i) x[i] += t * dx[i];
+    Cmul(s, x, zc);
+    codes_of(s, zc, cd);
+  }
+  return 0;
+}
+
 /* ---------------------------------------------------------------- one QP */
 void mpcqp_cpu_solve_one(const mpcqp_params* p, const double* model, double* u0, double* Xo, double* Uo,
                          int32_t* status, int32_t* iters, uint8_t* active) {
@@ -467,7 +591,7 @@ void mpcqp_cpu_solve_one(const mpcqp_params* p, const double* model, double* u0,
   double x[MAXNV], z[MAXR], y[MAXR];
   for (int i = 0; i < n; ++i) x[i] = 0.0;
   for (int r = 0; r < m; ++r) z[r] = y[r] = 0.0;
-  int admm_ok = 0, bad = 0;
+  int admm_ok = 0, bad = 0, polished = 0;
   /* non-finite problem data (NaN/inf in x0, ref, u_prev) -> numerical error, as k_setup */
   for (int i = 0; i < n && !bad; ++i) {
     if (!isfinite(s->q[i])) bad = 1;
@@ -481,12 +605,19 @@ void mpcqp_cpu_solve_one(const mpcqp_params* p, const double* model, double* u0,
     double rho = p->rho;
     const double sig = p->sigma, a = p->alpha;
     double rw[MAXR];
-    for (int r = 0; r < m; ++r) rw[r] = rho;
-    form_kkt(s, sig, rw, s->K);
-    ++n_fact;
-    if (sweep_inverse(n, s->K)) bad = 1;
-    double xt[MAXNV], zt[MAXR], rhs[MAXNV], tmp[MAXR], Ax[MAXR], Px[MAXNV], Aty[MAXNV];
+    int refactor = 1;
+    double xt[MAXNV], zt[MAXR], rhs[MAXNV], tmp[MAXR], Ax[MAXR], Px[MAXNV], Aty[MAXNV], xp[MAXNV];
     for (int it = 1; it <= p->max_iter && !bad; ++it) {
+      if (refactor) {
+        for (int r = 0; r < m; ++r) rw[r] = rho;
+        form_kkt(s, sig, rw, s->K);
+        ++n_fact;
+        if (sweep_inverse(n, s->K)) {
+          bad = 1;
+          break;
+        }
+        refactor = 0;
+      }
       for (int r = 0; r < m; ++r) tmp[r] = rho * z[r] - y[r];
       CTmul(s, tmp, rhs);
       for (int i = 0; i < n; ++i) rhs[i] += sig * x[i] - s->q[i];
@@ -548,6 +679,21 @@ void mpcqp_cpu_solve_one(const mpcqp_params* p, const double* model, double* u0,
           admm_ok = 1;
           break;
         }
+        /* early polish: an exact optimum found now satisfies the termination test itself */
+        if (p->polish && p->polish_from > 0 && it >= p->polish_from && it < p->max_iter) {
+          memcpy(xp, x, sizeof(double) * n);
+          const int pr_ = polish_run(s, xp, z, p->polish_attempt_max_iter, &pol_it, &n_fact, &n_ls);
+          if (pr_ < 0) {
+            bad = 1;
+            break;
+          }
+          if (pr_ > 0) {
+            memcpy(x, xp, sizeof(double) * n);
+            polished = 1;
+            break;
+          }
+          refactor = 1; /* the attempt used the inverse's storage */
+        }
         if (p->adaptive_rho && it % p->adaptive_rho_interval == 0) {
           const double pn = spr / (fmax(snAx, snz) + DIV_TOL);
           const double dn = sdu / (fmax(fmax(snPx, snAty), snq) + DIV_TOL);
@@ -555,10 +701,7 @@ void mpcqp_cpu_solve_one(const mpcqp_params* p, const double* model, double* u0,
           rn = fmin(fmax(rn, RHO_MIN), RHO_MAX);
           if (rn > rho * p->adaptive_rho_tolerance || rn < rho / p->adaptive_rho_tolerance) {
             rho = rn;
-            for (int r = 0; r < m; ++r) rw[r] = rho;
-            form_kkt(s, sig, rw, s->K);
-            ++n_fact;
-            if (sweep_inverse(n, s->K)) bad = 1;
+            refactor = 1;
           }
         }
       }
@@ -566,96 +709,19 @@ void mpcqp_cpu_solve_one(const mpcqp_params* p, const double* model, double* u0,
     st = admm_ok ? MPCQP_SOLVED : MPCQP_MAX_ITER_REACHED;
   }
 
-  /* ---- polish: semismooth Newton / active-set iteration on the scaled problem ---- */
-  const int do_polish = (p->method == MPCQP_METHOD_NEWTON) || p->polish;
+  /* ---- polish after ADMM (first guess: the ADMM z iterate), or from x = 0 (method newton) ---- */
+  const int do_polish = ((p->method == MPCQP_METHOD_NEWTON) || p->polish) && !polished;
   double xa[MAXNV];
   memcpy(xa, x, sizeof(double) * n);
-  if (do_polish && !bad) {
-    int pol_ok = 0;
-    uint8_t cd[MAXR], cn[MAXR];
-    double zc[MAXR], rw[MAXR], tmp[MAXR], rhs[MAXNV], xn[MAXNV], res[MAXNV], dx[MAXNV], Px[MAXNV], Pd[MAXNV],
-        zd[MAXR];
+  if (polished) {
+    st = MPCQP_SOLVED;
+  } else if (do_polish && !bad) {
+    double zc[MAXR];
     Cmul(s, x, zc);
-    /* first active-set guess: the ADMM z iterate (the prox output) when there was an ADMM phase,
-       else the rows of C x; later guesses classify C x */
-    codes_of(s, p->method == MPCQP_METHOD_ADMM ? z : zc, cd);
-    for (int it = 1; it <= p->polish_max_iter; ++it) {
-      pol_it = it;
-      for (int r = 0; r < m; ++r) {
-        rw[r] = cd[r] ? 2.0 * s->w[r] : 0.0;
-        tmp[r] = cd[r] == 2 ? rw[r] * s->u[r] : (cd[r] == 1 ? rw[r] * s->l[r] : 0.0);
-      }
-      form_kkt(s, 0.0, rw, s->M);
-      ++n_fact;
-      memcpy(s->K, s->M, sizeof(s->M));
-      if (sweep_inverse(n, s->K)) {
-        bad = 1;
-        break;
-      }
-      CTmul(s, tmp, rhs);
-      for (int i = 0; i < n; ++i) rhs[i] -= s->q[i];
-      matvec(n, s->K, rhs, xn);
-      /* one step of iterative refinement */
-      matvec(n, s->M, xn, res);
-      for (int i = 0; i < n; ++i) res[i] = rhs[i] - res[i];
-      matvec(n, s->K, res, dx);
-      for (int i = 0; i < n; ++i) xn[i] += dx[i];
-      double zn[MAXR];
-      Cmul(s, xn, zn);
-      codes_of(s, zn, cn);
-      int nonfinite = 0;
-      for (int i = 0; i < n; ++i) nonfinite |= !isfinite(xn[i]);
-      if (nonfinite) {
-        bad = 1;
-        break;
-      }
-      if (memcmp(cn, cd, m) == 0) {
-        memcpy(x, xn, sizeof(double) * n);
-        pol_ok = 1;
-        break;
-      }
-      /* exact line search along d = xn - x: phi(t) = f(x + t d) is convex piecewise quadratic, its
-         derivative piecewise linear and nondecreasing; semismooth Newton on phi' from t = 1
-         downwards reaches the minimizer in [0, 1] in a few pieces */
-      for (int i = 0; i < n; ++i) dx[i] = xn[i] - x[i];
-      matvec(n, s->P, x, Px);
-      matvec(n, s->P, dx, Pd);
-      for (int r = 0; r < m; ++r) zd[r] = zn[r] - zc[r];
-      double qd = 0.0, lin = 0.0;
-      for (int i = 0; i < n; ++i) {
-        qd += dx[i] * Pd[i];
-        lin += (Px[i] + s->q[i]) * dx[i];
-      }
-      double t = 1.0;
-      for (int ls = 0; ls < 40; ++ls) {
-        ++n_ls;
-        double d1 = lin + t * qd, d2 = qd;
-        for (int r = 0; r < m; ++r) {
-          const double zt = zc[r] + t * zd[r];
-          const double rr = zt > s->u[r] ? zt - s->u[r] : (zt < s->l[r] ? zt - s->l[r] : 0.0);
-          d1 += 2.0 * s->w[r] * rr * zd[r];
-          if (rr != 0.0) d2 += 2.0 * s->w[r] * zd[r] * zd[r];
-        }
-        if (d1 <= 0.0 || !(d2 > 0.0)) break;
-        const double tn = fmax(0.0, t - d1 / d2);
-        if (tn >= t) break;
-        /* same linear piece of phi' at tn as at t: tn is that piece's root, the minimizer */
-        int same = 1;
-        for (int r = 0; r < m && same; ++r) {
-          const double za = zc[r] + t * zd[r], zb = zc[r] + tn * zd[r];
-          const int ca = za > s->u[r] ? 2 : (za < s->l[r] ? 1 : 0);
-          const int cb = zb > s->u[r] ? 2 : (zb < s->l[r] ? 1 : 0);
-          same = ca == cb;
-        }
-        t = tn;
-        if (same) break;
-      }
-      for (int i = 0; i < n; ++i) x[i] += t * dx[i];
-      for (int r = 0; r < m; ++r) zc[r] = zc[r] + t * zd[r];
-      Cmul(s, x, zc);
-      codes_of(s, zc, cd);
-    }
-    if (pol_ok)
+    const int r_ = polish_run(s, x, p->method == MPCQP_METHOD_ADMM ? z : zc, p->polish_max_iter, &pol_it, &n_fact, &n_ls);
+    if (r_ < 0)
+      bad = 1;
+    else if (r_ > 0)
       st = MPCQP_SOLVED;
     else if (p->method == MPCQP_METHOD_ADMM) {
       memcpy(x, xa, sizeof(double) * n);
@@ -666,9 +732,13 @@ void mpcqp_cpu_solve_one(const mpcqp_params* p, const double* model, double* u0,
   for (int i = 0; i < n; ++i) bad |= !isfinite(x[i]);
   if (bad) st = MPCQP_NUMERICAL_ERROR;
 
-  /* ---- outputs (unscaled) ---- */
-  double U[MAXNV];
-  for (int i = 0; i < n; ++i) U[i] = s->D[i] * x[i];
+  /* ---- outputs (unscaled): speeds W -> accelerations, states by the LTV recursion ---- */
+  double W[MAXNV], U[MAXNV];
+  for (int i = 0; i < n; ++i) W[i] = s->D[i] * x[i];
+  for (int k = 0; k < N; ++k) {
+    U[2 * k] = (W[2 * k] - (k == 0 ? x0[3] : W[2 * k - 2])) / p->dt;
+    U[2 * k + 1] = W[2 * k + 1];
+  }
   double X[4][MAXN + 1];
   X[0][0] = x0[0];
   X[1][0] = x0[1];
@@ -679,7 +749,7 @@ void mpcqp_cpu_solve_one(const mpcqp_params* p, const double* model, double* u0,
     X[0][k + 1] = X[0][k] + al[k] * psi + be[k] * v + c0[k];
     X[1][k + 1] = X[1][k] + ga[k] * psi + et[k] * v + c1[k];
     X[2][k + 1] = psi + si[k] * U[2 * k + 1];
-    X[3][k + 1] = v + p->dt * U[2 * k];
+    X[3][k + 1] = W[2 * k];
   }
   if (u0) {
     u0[0] = U[0];

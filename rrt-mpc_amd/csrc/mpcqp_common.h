@@ -143,6 +143,8 @@ __device__ __forceinline__ double wave_max(double v) {  // v >= 0
 // lane i <- lane i-2 (0 for i < 2);  lane i <- lane i+2 (0 past the wave)
 __device__ __forceinline__ double shr2(double v) { return dpp<kWaveShr1>(dpp<kWaveShr1>(v)); }
 __device__ __forceinline__ double shl2(double v) { return dpp<kWaveShl1>(dpp<kWaveShl1>(v)); }
+__device__ __forceinline__ double shr4(double v) { return shr2(shr2(v)); }
+__device__ __forceinline__ double shl4(double v) { return shl2(shl2(v)); }
 __device__ __forceinline__ bool wave_any(bool b) { return __ballot(b) != 0ull; }
 
 // ---- register broadcasts for the dense row-per-lane products (no LDS)

@@ -18,7 +18,6 @@ struct SetupSmem {
 template <int N>
 struct SolveSmem {
   double P[4 * N * N];  // Pbar, row-major n x n (lane `col` reads column col: conflict-free)
-  double sv[N + 1];     // suffix sums of the v-row weights (form)
 };
 
 template <int N>
@@ -29,6 +28,13 @@ union SolveLds {
 
 // ------------------------------------------------------------------ shared solver context
 // Per-lane view of one scaled QP plus the structured operators and the KKT inverse.
+// Variables W = (v_1, delta_0, v_2, delta_1, ...): lane 2j holds the speed v_{j+1}, lane 2j+1
+// the steering delta_j.  The rows owned by lane p (slot 0: v row, p even; slot 1: input row;
+// slot 2: rate row) are banded in those variables:
+//   slot 0  v_{p/2+1}                                    (identity)
+//   slot 1  e1[0] t_p + e1[1] t_{p-2}                    (a_j = (v_{j+1} - v_j)/dt; delta_j)
+//   slot 2  e2[0] t_p + e2[1] t_{p-2} + e2[2] t_{p-4}    (a_j - a_{j-1}; delta_j - delta_{j-1})
+// with t = D x and e the row coefficients times the row scaling E.
 template <int N>
 struct Ctx {
   static constexpr int n = 2 * N;
@@ -37,21 +43,20 @@ struct Ctx {
   double dt;
   double D, qv;
   double E[3], lo[3], hi[3], wb[3];
+  double e1[2], e2[3];
   double cscale;
   const double* __restrict__ P;  // Pbar (LDS, row-major n x n)
-  double* sv;                    // LDS, N+1 doubles
   static constexpr int kNW = (n + 15) / 16;  // 16-lane rows holding the n variables
   // KKT inverse, row `lane`: A^{-1}[lane][j] = -r[j] (symmetric sweep operator)
   double r[n];
 
-  // Bind the context to this lane and the solve LDS (Pbar, broadcast buffers); the problem
-  // data fields are filled by setup_qp.
+  // Bind the context to this lane and the solve LDS (Pbar); the problem data fields are
+  // filled by setup_qp.
   __device__ __forceinline__ void init(int ln, double dt_, SolveSmem<N>& s) {
     lane = ln;
     act = ln < n;
     even = act && ((ln & 1) == 0);
     dt = dt_;
-    sv = s.sv;
     P = s.P;
   }
 
@@ -61,28 +66,29 @@ struct Ctx {
   __device__ __forceinline__ void opaque() {
     asm volatile("" : "+v"(D), "+v"(qv), "+v"(lane));
     asm volatile("" : "+v"(E[0]), "+v"(E[1]), "+v"(E[2]));
+    asm volatile("" : "+v"(e1[0]), "+v"(e1[1]), "+v"(e2[0]), "+v"(e2[1]), "+v"(e2[2]));
     asm volatile("" : "+v"(lo[0]), "+v"(lo[1]), "+v"(lo[2]));
     asm volatile("" : "+v"(hi[0]), "+v"(hi[1]), "+v"(hi[2]));
     asm volatile("" : "+v"(wb[0]), "+v"(wb[1]), "+v"(wb[2]));
   }
 
-  // z = Cbar x
+  // z = Cbar x: shifts only (no scans)
   __device__ __forceinline__ void Cmul(double x, double z[3]) const {
     const double t = D * x;
-    const double pre = scan_add(even ? t : 0.0, lane);
     const double tm2 = shr2(t);
-    z[0] = E[0] * dt * pre;
-    z[1] = E[1] * t;
-    z[2] = E[2] * (lane >= 2 ? t - tm2 : t);
+    const double tm4 = shr2(tm2);
+    z[0] = E[0] * t;
+    z[1] = e1[0] * t + e1[1] * tm2;
+    z[2] = (e2[0] * t + e2[1] * tm2) + e2[2] * tm4;
   }
   // x = Cbar' y
   __device__ __forceinline__ double CTmul(const double y[3]) const {
-    const double suf = rscan_add(E[0] * y[0], lane);
-    const double ey2 = E[2] * y[2];
-    const double n2 = shl2(ey2);
-    double t = (even ? dt * suf : 0.0) + E[1] * y[1] + ey2;
-    if (lane + 2 < n) t -= n2;
-    return act ? D * t : 0.0;
+    const double a = e1[1] * y[1] + e2[1] * y[2];  // to the variable 2 back
+    const double b = e2[2] * y[2];                 // to the variable 4 back
+    double t = (E[0] * y[0] + e1[0] * y[1]) + e2[0] * y[2];
+    t += shl2(a);
+    t += shl4(b);
+    return D * t;
   }
   // (Pbar v)_lane, Pbar symmetric: lane reads its row as a conflict-free column of the LDS copy
   __device__ __forceinline__ double Pmul(double v) const {
@@ -96,38 +102,30 @@ struct Ctx {
     });
     return act ? (a[0] + a[1]) + (a[2] + a[3]) : 0.0;
   }
-  // KKT matrix A = Pbar + s I + Cbar' diag(rw) Cbar, row `lane` -> r[]
+  // KKT matrix A = Pbar + s I + Cbar' diag(rw) Cbar, row `lane` -> r[].  The row part is a
+  // band (lanes p-4 .. p+4 of the same kind): its five entries per lane come from shifts.
   __device__ __forceinline__ void form(double s, const double rw[3]) {
     // opaque lane copy: keeps per-column masks/addresses from being hoisted out of solver loops
     int ln = lane;
     asm volatile("" : "+v"(ln));
-    const bool ev_ln = ln < n && (ln & 1) == 0;
-    const double ev = E[0] * E[0] * rw[0];
-    const double suf = rscan_add(even ? ev : 0.0, lane);  // sum over v rows >= lane/2
-    const double du2 = E[2] * E[2] * rw[2];
-    const double du2n = shl2(du2);
-    lds_sync();
-    if (even) sv[lane >> 1] = suf;
-    lds_sync();
-    double diag = E[1] * E[1] * rw[1] + du2;
-    if (ln + 2 < n) diag += du2n;
+    const double a1 = rw[1] * e1[1], a2 = rw[2] * e2[1], b2 = rw[2] * e2[2];
+    const double dg = (E[0] * E[0] * rw[0] + rw[1] * e1[0] * e1[0]) + rw[2] * e2[0] * e2[0];
+    const double diag = dg + shl2(a1 * e1[1] + a2 * e2[1]) + shl4(b2 * e2[2]);
+    const double up2 = shl2(a1 * e1[0] + a2 * e2[0]) + shl4(b2 * e2[1]);  // entry (p, p+2)
+    const double up4 = shl4(b2 * e2[0]);                                  // entry (p, p+4)
+    const double b0 = D * D * diag + s;
+    const double bp2 = D * shl2(D) * up2, bp4 = D * shl4(D) * up4;
+    const double bm2 = shr2(bp2), bm4 = shr4(bp4);  // symmetric: (p, p-2) = lane p-2's (., +2)
     const int col = ln < n ? ln : 0;
-    const double Dm = ln < n ? D : 0.0;
-    double wD[4];
-    bcast<kNW>(Dm, wD);  // D_j of every lane j
-    // v-row weight sums sv[max(lane, j) / 2]: the lane's own entry for j <= lane (one read),
-    // a wave-uniform entry for j > lane
-    const double sv_own = ev_ln ? sv[ln >> 1] : 0.0;
     Unroll<0, n>::run([&](auto jc) {
       constexpr int j = decltype(jc)::value;
       double t = 0.0;
-      if ((j & 1) == 0 && ev_ln) t = dt * dt * (ln > j ? sv_own : sv[j >> 1]);
-      if (j == ln) t += diag;
-      if (j == ln + 2) t -= du2n;
-      if (j + 2 == ln) t -= du2;
-      double v = ln < n ? P[j * n + col] + (j == ln ? s : 0.0) : 0.0;
-      fmac_bc<j % 16>(v, wD[j / 16], Dm * t);
-      r[j] = v;
+      if (j == ln) t = b0;
+      if (j == ln + 2) t = bp2;
+      if (j + 2 == ln) t = bm2;
+      if (j == ln + 4) t = bp4;
+      if (j + 4 == ln) t = bm4;
+      r[j] = ln < n ? P[j * n + col] + t : 0.0;
     });
   }
   // Symmetric sweep operator on the rows in r[]: afterwards A^{-1} = -r (row `lane`).
@@ -169,15 +167,12 @@ struct Ctx {
   // kappa = delta / (1 + delta c'u).  Used by the polish when a few soft rows enter or leave
   // the active set.  false (inverse untouched) when 1 + delta c'u is not safely positive.
   __device__ __forceinline__ bool rank1(int tau, int l, double delta) {
-    const double e = readlane(tau == 0 ? E[0] : (tau == 1 ? E[1] : E[2]), l);
-    double c = 0.0;
-    if (tau == 0)
-      c = (even && lane <= l) ? e * dt * D : 0.0;
-    else if (tau == 1)
-      c = lane == l ? e * D : 0.0;
-    else
-      c = lane == l ? e * D : (lane + 2 == l ? -e * D : 0.0);
-    if (!act) c = 0.0;
+    // the row's coefficients on the variables l, l-2, l-4 (lane l's e)
+    const double c0 = readlane(tau == 0 ? E[0] : (tau == 1 ? e1[0] : e2[0]), l);
+    const double c1 = readlane(tau == 1 ? e1[1] : (tau == 2 ? e2[1] : 0.0), l);
+    const double c2 = readlane(tau == 2 ? e2[2] : 0.0, l);
+    double c = lane == l ? c0 : (lane + 2 == l ? c1 : (lane + 4 == l ? c2 : 0.0));
+    c = act ? c * D : 0.0;
     const double u = inv_mul(c);
     const double den = 1.0 + delta * wave_sum(c * u);
     if (!(den > kRank1Min) || !isfinite(den)) return false;
@@ -208,10 +203,12 @@ struct Ctx {
 // problem on chip for the later phases: Pbar (symmetric, row-major) in the solve LDS, the
 // per-lane data in C.  Returns true on non-finite problem data.  dbg (debug_state builds of
 // the parameter block only) receives the solver state for inspection.
-// Row slots owned by lane p (p < n = 2N):
-//   slot 0: v row (p even): v_{p/2+1} - v0 = dt * sum_{j<=p/2} a_j   (mpc_controller.py:81-82,115-116)
-//   slot 1: input row        U_p                                      (:83-86)
-//   slot 2: rate row         U_p - U_{p-2} (u_prev at k = 0)          (:89-106)
+// Variables W = (v_1, delta_0, v_2, delta_1, ...) (a_k = (v_{k+1} - v_k)/dt: a bijective affine
+// change of the reference's U, same optimum).  Row slots owned by lane p (p < n = 2N):
+//   slot 0: v row (p even): v_{p/2+1}                                  (mpc_controller.py:81-82,115-116)
+//   slot 1: input row        a_{p/2} or delta_{p/2}                    (:83-86)
+//   slot 2: rate row         U_p - U_{p-2} (u_prev at k = 0)           (:89-106)
+// the constant parts (v_0 = x0[3], u_prev) moved into the bounds.
 template <int N>
 __device__ __forceinline__ bool setup_qp(const mpcqp_params& p, int b, const double* __restrict__ model, Ctx<N>& C,
                                          SolveLds<N>& lds, double* __restrict__ scratch, double* __restrict__ dbg) {
@@ -253,17 +250,18 @@ __device__ __forceinline__ bool setup_qp(const mpcqp_params& p, int b, const dou
       acc += a[k];
       sm.pre[lane][k + 1] = acc;
     }
-  } else if (lane == 4) {
+  } else if (lane == 4) {  // free response at W = 0: v_k = 0 for k >= 1, constant heading
     double px = x0[0], py = x0[1];
-    const double psi = x0[2], v = x0[3];
+    const double psi = x0[2];
     for (int m = 1; m <= N; ++m) {
       const int k = m - 1;
+      const double v = k == 0 ? x0[3] : 0.0;
       px = px + al[k] * psi + be[k] * v + c0[k];
       py = py + ga[k] * psi + et[k] * v + c1[k];
       sm.err[m][0] = px - rr[4 * m + 0];
       sm.err[m][1] = py - rr[4 * m + 1];
       sm.err[m][2] = psi - rr[4 * m + 2];
-      sm.err[m][3] = v - rr[4 * m + 3];
+      sm.err[m][3] = 0.0 - rr[4 * m + 3];
     }
   }
   __syncthreads();
@@ -289,9 +287,9 @@ __device__ __forceinline__ bool setup_qp(const mpcqp_params& p, int b, const dou
     const int j = lane >> 1;
     const bool gcol = lane == n;
     const double sj = gcol ? 0.0 : si[j];
-    const double pa0 = gcol ? 0.0 : sm.pre[0][j + 1], pb0 = gcol ? 0.0 : sm.pre[1][j + 1];
-    const double pg0 = gcol ? 0.0 : sm.pre[2][j + 1], pe0 = gcol ? 0.0 : sm.pre[3][j + 1];
-    double mu0 = 0.0, mu1 = 0.0, mu2 = 0.0, mu3 = 0.0;
+    const double pa0 = gcol ? 0.0 : sm.pre[0][j + 1], pg0 = gcol ? 0.0 : sm.pre[2][j + 1];
+    const double bj = (!gcol && j + 1 < N) ? be[j + 1] : 0.0, ej = (!gcol && j + 1 < N) ? et[j + 1] : 0.0;
+    double mu0 = 0.0, mu1 = 0.0, mu2 = 0.0;
 #pragma unroll
     for (int m = N; m >= 1; --m) {
       double s0, s1, s2, s3;
@@ -301,11 +299,11 @@ __device__ __forceinline__ bool setup_qp(const mpcqp_params& p, int b, const dou
         s2 = sm.err[m][2];
         s3 = sm.err[m][3];
       } else if (m > j) {
-        if (cc == 0) {
-          s0 = dt * (sm.pre[1][m] - pb0);
-          s1 = dt * (sm.pre[3][m] - pe0);
+        if (cc == 0) {  // v_{j+1}: itself at m = j+1, the positions from m = j+2 on
+          s0 = m >= j + 2 ? bj : 0.0;
+          s1 = m >= j + 2 ? ej : 0.0;
           s2 = 0.0;
-          s3 = dt;
+          s3 = m == j + 1 ? 1.0 : 0.0;
         } else {
           s0 = sj * (sm.pre[0][m] - pa0);
           s1 = sj * (sm.pre[2][m] - pg0);
@@ -321,19 +319,21 @@ __device__ __forceinline__ bool setup_qp(const mpcqp_params& p, int b, const dou
       const double w1 = W(1, 0) * s0 + W(1, 1) * s1 + W(1, 2) * s2 + W(1, 3) * s3;
       const double w2 = W(2, 0) * s0 + W(2, 1) * s1 + W(2, 2) * s2 + W(2, 3) * s3;
       const double w3 = W(3, 0) * s0 + W(3, 1) * s1 + W(3, 2) * s2 + W(3, 3) * s3;
+      // row v_m: its own cost term + the positions after it; row delta_{m-1}: si * heading adjoint
+      double ha;
       if (m < N) {
         const double m0 = mu0, m1 = mu1;
+        ha = w3 + (be[m] * m0 + et[m] * m1);
         mu0 = w0 + m0;
         mu1 = w1 + m1;
         mu2 = w2 + (mu2 + al[m] * m0 + ga[m] * m1);
-        mu3 = w3 + (mu3 + be[m] * m0 + et[m] * m1);
       } else {
+        ha = w3;
         mu0 = w0;
         mu1 = w1;
         mu2 = w2;
-        mu3 = w3;
       }
-      const double ha = dt * mu3, hd = si[m - 1] * mu2;
+      const double hd = si[m - 1] * mu2;
       if (gcol) {
         sm.g[2 * (m - 1)] = ha;
         sm.g[2 * (m - 1) + 1] = hd;
@@ -342,15 +342,29 @@ __device__ __forceinline__ bool setup_qp(const mpcqp_params& p, int b, const dou
         Pc[2 * (m - 1) + 1] = hd;
       }
     }
-    if (!gcol) {
-      const double R0 = 0.5 * (p.r[0 * 2 + cc] + p.r[cc * 2 + 0]);
-      const double R1 = 0.5 * (p.r[1 * 2 + cc] + p.r[cc * 2 + 1]);
+    // input cost sum_k U_k' R U_k with a_k = (v_{k+1} - v_k)/dt: a band of column `lane`
+    const double r00 = 0.5 * (p.r[0] + p.r[0]) / (dt * dt), r10 = 0.5 * (p.r[2] + p.r[1]) / dt;
+    const double r11 = 0.5 * (p.r[3] + p.r[3]);
+    if (gcol) {  // the v_0 = x0[3] end of a_0
+      sm.g[0] += -x0[3] * r00;
+      sm.g[1] += -x0[3] * r10;
+    } else {
 #pragma unroll
-      for (int i = 0; i < n; i += 2)
-        if (i == 2 * j) {
-          Pc[i] += R0;
-          Pc[i + 1] += R1;
+      for (int i = 0; i < n; ++i) {
+        const int d = i - lane;
+        double add = 0.0;
+        if (cc == 0) {
+          if (d == 0) add = lane + 2 < n ? 2.0 * r00 : r00;
+          if (d == 2 || d == -2) add = -r00;
+          if (d == 1) add = r10;
+          if (d == 3) add = -r10;
+        } else {
+          if (d == 0) add = r11;
+          if (d == -1) add = r10;
+          if (d == -3) add = -r10;
         }
+        Pc[i] += add;
+      }
     }
   }
   __syncthreads();
@@ -369,16 +383,26 @@ __device__ __forceinline__ bool setup_qp(const mpcqp_params& p, int b, const dou
     cmax = fmax(cmax, fabs(Pc[i]));
   }
   double lo[3], hi[3], wt[3], E[3];
+  // unscaled row coefficients (slot 1: own, 2 back; slot 2: own, 2 back, 4 back)
+  const double idt = 1.0 / dt, v0 = x0[3];
+  double k1[2], k2[3];
+  k1[0] = act ? (even ? idt : 1.0) : 0.0;
+  k1[1] = (even && lane >= 2) ? -idt : 0.0;
+  k2[0] = act ? (even ? idt : 1.0) : 0.0;
+  k2[1] = act ? (even ? (lane >= 2 ? -2.0 * idt : 0.0) : (lane >= 3 ? -1.0 : 0.0)) : 0.0;
+  k2[2] = (even && lane >= 4) ? idt : 0.0;
   {
-    const double off = lane < 2 ? up[cc] : 0.0;
-    lo[0] = even ? p.v_bounds[0] - x0[3] : 0.0;
-    hi[0] = even ? p.v_bounds[1] - x0[3] : 0.0;
+    // the rows' constant parts moved into the bounds: a_0 = (v_1 - v_0)/dt, a_1 - a_0 carries +v_0/dt
+    const double ofa = lane == 0 ? v0 * idt : 0.0;
+    const double ofr = lane < 2 ? up[cc] + ofa : (lane == 2 ? -v0 * idt : 0.0);
+    lo[0] = even ? p.v_bounds[0] : 0.0;
+    hi[0] = even ? p.v_bounds[1] : 0.0;
     wt[0] = even ? p.slack_velocity : 0.0;
-    lo[1] = act ? p.u_bounds[2 * cc] : 0.0;
-    hi[1] = act ? p.u_bounds[2 * cc + 1] : 0.0;
+    lo[1] = act ? p.u_bounds[2 * cc] + ofa : 0.0;
+    hi[1] = act ? p.u_bounds[2 * cc + 1] + ofa : 0.0;
     wt[1] = act ? p.slack_input : 0.0;
-    lo[2] = act ? p.du_bounds[2 * cc] + off : 0.0;
-    hi[2] = act ? p.du_bounds[2 * cc + 1] + off : 0.0;
+    lo[2] = act ? p.du_bounds[2 * cc] + ofr : 0.0;
+    hi[2] = act ? p.du_bounds[2 * cc + 1] + ofr : 0.0;
     wt[2] = act ? p.slack_rate : 0.0;
     E[0] = even ? 1.0 : 0.0;
     E[1] = act ? 1.0 : 0.0;
@@ -391,20 +415,20 @@ __device__ __forceinline__ bool setup_qp(const mpcqp_params& p, int b, const dou
 
   // ---- Ruiz equilibration + cost scaling (OSQP scale_data, `scaling` iterations) ----
   for (int it = 0; it < p.scaling; ++it) {
-    // column norms of [P; A] (first n columns of the KKT matrix)
-    const double sufE = rscan_max(E[0], lane);  // max E over v rows >= p/2 (odd lanes carry 0)
-    const double e2n = shl2(E[2]);
-    double ccol = fmax(E[1], E[2]);
-    if (lane + 2 < n) ccol = fmax(ccol, e2n);
-    if (even) ccol = fmax(ccol, dt * sufE);
+    // column norms of [P; A] (first n columns of the KKT matrix): the lane's own rows and
+    // the banded rows 2 and 4 ahead
+    double ccol = fmax(fmax(E[0], E[1] * fabs(k1[0])), E[2] * fabs(k2[0]));
+    ccol = fmax(ccol, shl2(fmax(E[1] * fabs(k1[1]), E[2] * fabs(k2[1]))));
+    ccol = fmax(ccol, shl4(E[2] * fabs(k2[2])));
     ccol *= D;
     const double dl = act ? 1.0 / sqrt(limit_scaling(fmax(cmax, ccol))) : 0.0;
     // row norms of A
-    const double preD = scan_max(even ? D : 0.0, lane);
-    const double Dm2 = shr2(D);
-    const double el0 = even ? 1.0 / sqrt(limit_scaling(E[0] * dt * preD)) : 0.0;
-    const double el1 = act ? 1.0 / sqrt(limit_scaling(E[1] * D)) : 0.0;
-    const double el2 = act ? 1.0 / sqrt(limit_scaling(E[2] * (lane >= 2 ? fmax(D, Dm2) : D))) : 0.0;
+    const double Dm2 = shr2(D), Dm4 = shr2(Dm2);
+    const double r1 = fmax(fabs(k1[0]) * D, fabs(k1[1]) * Dm2);
+    const double r2 = fmax(fmax(fabs(k2[0]) * D, fabs(k2[1]) * Dm2), fabs(k2[2]) * Dm4);
+    const double el0 = even ? 1.0 / sqrt(limit_scaling(E[0] * D)) : 0.0;
+    const double el1 = act ? 1.0 / sqrt(limit_scaling(E[1] * r1)) : 0.0;
+    const double el2 = act ? 1.0 / sqrt(limit_scaling(E[2] * r2)) : 0.0;
     // apply: P <- dl P dl (column `lane`, the row factors read back from LDS), q <- dl q
     lds_sync();
     sm.buf[lane] = dl;
@@ -464,6 +488,11 @@ __device__ __forceinline__ bool setup_qp(const mpcqp_params& p, int b, const dou
   C.qv = qv;
   C.D = D;
   C.cscale = cscale;
+  C.e1[0] = E[1] * k1[0];
+  C.e1[1] = E[1] * k1[1];
+  C.e2[0] = E[2] * k2[0];
+  C.e2[1] = E[2] * k2[1];
+  C.e2[2] = E[2] * k2[2];
 #pragma unroll
   for (int r = 0; r < 3; ++r) {
     C.E[r] = E[r];
@@ -501,20 +530,176 @@ __device__ __forceinline__ bool setup_qp(const mpcqp_params& p, int b, const dou
   return bad_input;
 }
 
+// ------------------------------------------------------------------ K2c: polish
+// Semismooth Newton / active-set iteration on the scaled problem from x (in/out): the first
+// active-set guess classifies zg, later ones C x.  Each pass factorizes the Newton matrix of
+// the current set (from scratch, or by rank-1 updates of the previous pass's inverse when few
+// soft rows changed), solves with one step of iterative refinement, and stops when the set
+// reproduces itself (the exact optimum: returns 1, x = that optimum); otherwise an exact line
+// search along the Newton step.  0: not found within max_it passes, -1: numerical failure.
+// Uses the KKT inverse registers (an ADMM phase that continues must refactor).
+template <int N>
+__device__ __forceinline__ int polish_qp(Ctx<N>& C, double& x, const double zg[3], int max_it, int& pol_it,
+                                         int& nfact, int& n_ls) {
+  constexpr int n = 2 * N;
+  const bool act = C.act;
+  int result = 0;
+  Stamps T;
+  double zc[3];
+  int cd[3];
+  C.Cmul(x, zc);
+#pragma unroll
+  for (int r = 0; r < 3; ++r) cd[r] = zg[r] > C.hi[r] ? 2 : (zg[r] < C.lo[r] ? 1 : 0);
+  constexpr int kMaxRank1 = n / 2;  // more changed rows than this: refactor (form + sweep)
+  double rwf[3] = {0.0, 0.0, 0.0};  // soft-row weights of the current factorization
+  bool have_fact = false;
+  for (int pass = 0; pass < max_it; ++pass) {
+    ++pol_it;
+    C.opaque();
+    double rw[3], tmp[3];
+#pragma unroll
+    for (int r = 0; r < 3; ++r) {
+      rw[r] = cd[r] ? 2.0 * C.wb[r] : 0.0;
+      tmp[r] = cd[r] == 2 ? rw[r] * C.hi[r] : (cd[r] == 1 ? rw[r] * C.lo[r] : 0.0);
+    }
+    // Factorize the Newton matrix of this active set: from scratch on the first pass, by
+    // rank-1 updates of the previous inverse when only a few soft rows changed.
+    bool refac = !have_fact;
+    if (!refac) {
+      uint64_t chg[3];
+      int nchg = 0;
+#pragma unroll
+      for (int r = 0; r < 3; ++r) {
+        chg[r] = __ballot(act && rw[r] != rwf[r]);
+        nchg += __popcll(chg[r]);
+      }
+      refac = nchg > kMaxRank1;
+      T.begin();
+#pragma unroll
+      for (int r = 0; r < 3; ++r) {
+        uint64_t m = chg[r];
+        while (m && !refac) {
+          const int l = __builtin_ctzll(m);
+          m &= m - 1;
+          refac = !C.rank1(r, l, readlane(rw[r] - rwf[r], l));
+        }
+      }
+      T.end(1);
+    }
+    if (refac) {
+      T.begin();
+      C.form(0.0, rw);
+      T.end(0);
+      T.begin();
+      const bool okf = C.sweep();
+      T.end(1);
+      if (wave_any(!okf)) {
+        result = -1;
+        break;
+      }
+      have_fact = true;
+    }
+    ++nfact;
+#pragma unroll
+    for (int r = 0; r < 3; ++r) rwf[r] = rw[r];
+    T.begin();
+    const double rhs = C.CTmul(tmp) - C.qv;
+    double xn = C.inv_mul(rhs);
+    {  // one step of iterative refinement: res = rhs - M xn
+      double zz[3], t3[3];
+      C.Cmul(xn, zz);
+#pragma unroll
+      for (int r = 0; r < 3; ++r) t3[r] = rw[r] * zz[r];
+      const double Mx = C.Pmul(xn) + C.CTmul(t3);
+      xn += C.inv_mul(rhs - Mx);
+    }
+    double zn[3];
+    C.Cmul(xn, zn);
+    bool diff = false;
+#pragma unroll
+    for (int r = 0; r < 3; ++r) {
+      const int c2 = zn[r] > C.hi[r] ? 2 : (zn[r] < C.lo[r] ? 1 : 0);
+      diff = diff || (c2 != cd[r]);
+    }
+    T.end(2);
+    if (wave_any(!isfinite(xn))) {
+      result = -1;
+      break;
+    }
+    if (!wave_any(diff)) {
+      x = xn;
+      result = 1;
+      break;
+    }
+    // exact line search along d = xn - x: phi(t) = f(x + t d) is convex piecewise quadratic,
+    // phi' piecewise linear and nondecreasing; semismooth Newton on phi' from t = 1 downwards
+    // lands on the minimizer in [0, 1] after a few pieces (two independent reductions a step)
+    T.begin();
+    const double dx = act ? xn - x : 0.0;
+    const double Px = C.Pmul(x);
+    const double Pd = C.Pmul(dx);
+    double zd[3];
+#pragma unroll
+    for (int r = 0; r < 3; ++r) zd[r] = zn[r] - zc[r];
+    const double qd = wave_sum(act ? dx * Pd : 0.0);
+    const double lin = wave_sum(act ? (Px + C.qv) * dx : 0.0);
+    double t = 1.0;
+    for (int ls = 0; ls < 40; ++ls) {
+      ++n_ls;
+      double g1 = 0.0, g2 = 0.0;
+#pragma unroll
+      for (int r = 0; r < 3; ++r) {
+        const double zt = zc[r] + t * zd[r];
+        const double rr = zt > C.hi[r] ? zt - C.hi[r] : (zt < C.lo[r] ? zt - C.lo[r] : 0.0);
+        g1 += 2.0 * C.wb[r] * rr * zd[r];
+        if (rr != 0.0) g2 += 2.0 * C.wb[r] * zd[r] * zd[r];
+      }
+      const double d1 = lin + t * qd + wave_sum(g1);
+      const double d2 = qd + wave_sum(g2);
+      if (d1 <= 0.0 || !(d2 > 0.0)) break;
+      const double tn = fmax(0.0, t - d1 / d2);
+      if (tn >= t) break;
+      // same linear piece of phi' at tn as at t: tn is that piece's root, the minimizer
+      bool moved = false;
+#pragma unroll
+      for (int r = 0; r < 3; ++r) {
+        const double za = zc[r] + t * zd[r], zb = zc[r] + tn * zd[r];
+        const int ca = za > C.hi[r] ? 2 : (za < C.lo[r] ? 1 : 0);
+        const int cb = zb > C.hi[r] ? 2 : (zb < C.lo[r] ? 1 : 0);
+        moved = moved || ca != cb;
+      }
+      t = tn;
+      if (!wave_any(moved)) break;
+    }
+    x = x + t * dx;
+    C.Cmul(x, zc);
+#pragma unroll
+    for (int r = 0; r < 3; ++r) cd[r] = zc[r] > C.hi[r] ? 2 : (zc[r] < C.lo[r] ? 1 : 0);
+    T.end(3);
+  }
+  T.flush(8);  // g_stamps[8..11]: polish form, sweep/rank-1, solve+check, line search
+  return result;
+}
+
 // ------------------------------------------------------------------ K2b: ADMM
-// Returns the ADMM flag (-1 numerical error, 0 not converged, 1 converged); x, it, nfact out.
+// OSQP's iteration on the scaled problem (rho / sigma / alpha / adaptive rho / termination as
+// the reference settings).  From iteration polish_from on, a termination check that fails also
+// attempts the polish: an exact optimum found there satisfies the termination test itself.
+// Returns the ADMM flag (-1 numerical error, 0 not converged, 1 converged, 2 solved by an early
+// polish); x, z, the counters out.
 template <int N>
 __device__ __forceinline__ int admm_qp(const mpcqp_params& p, Ctx<N>& C, bool bad, double& x_out, double z_out[3],
-                                       int& it_out, int& nfact_out, double* __restrict__ dbg) {
+                                       int& it_out, int& nfact_out, int& pol_it, int& n_ls, double* __restrict__ dbg) {
   const bool act = C.act;
   double x = 0.0, z[3] = {0.0, 0.0, 0.0}, y[3] = {0.0, 0.0, 0.0};
   double rho = p.rho;
   const double sg = p.sigma, alpha = p.alpha;
-  bool ok = false;
+  bool ok = false, polished = false;
   int it = 0, nfact = 0;
+  const bool early = p.polish != 0 && p.polish_from > 0;
   Stamps T, T2;
   T2.begin();
-  while (it < p.max_iter && !bad && !ok) {
+  while (it < p.max_iter && !bad && !ok && !polished) {
     {
       const double rw[3] = {rho, rho, rho};
       T.begin();
@@ -613,6 +798,20 @@ __device__ __forceinline__ int admm_qp(const mpcqp_params& p, Ctx<N>& C, bool ba
           ok = true;
           break;
         }
+        if (early && it >= p.polish_from && it < p.max_iter) {
+          double xp = x;
+          const int pr_ = polish_qp<N>(C, xp, z, p.polish_attempt_max_iter, pol_it, nfact, n_ls);
+          if (pr_ < 0) {
+            bad = true;
+            break;
+          }
+          if (pr_ > 0) {
+            x = xp;
+            polished = true;
+            break;
+          }
+          refactor = true;  // the attempt used the inverse's registers
+        }
         if (p.adaptive_rho && it % p.adaptive_rho_interval == 0) {
           const double pn = spr / (snprim + kDivTol);
           const double dn = sdu / (sndual + kDivTol);
@@ -626,11 +825,12 @@ __device__ __forceinline__ int admm_qp(const mpcqp_params& p, Ctx<N>& C, bool ba
       }
     }
   }
+  const int flag = bad ? -1 : (polished ? 2 : (ok ? 1 : 0));
   if (dbg) {
     dbg[state_lane_off(N) + kFx * kWave + threadIdx.x] = act ? x : 0.0;
     if (threadIdx.x == 0) {
       double* sc = dbg + state_scal_off(N);
-      sc[1] = bad ? -1.0 : (ok ? 1.0 : 0.0);
+      sc[1] = flag < 0 ? -1.0 : (flag > 0 ? 1.0 : 0.0);
       sc[2] = (double)it;
       sc[3] = (double)nfact;
     }
@@ -643,172 +843,43 @@ __device__ __forceinline__ int admm_qp(const mpcqp_params& p, Ctx<N>& C, bool ba
   T2.end(0);
   T.flush(0);   // g_stamps[0..3]: form, sweep, ADMM iteration body, termination checks
   T2.flush(4);  // g_stamps[4]: whole ADMM phase
-  return bad ? -1 : (ok ? 1 : 0);
+  return flag;
 }
 
 // ------------------------------------------------------------------ K2c: polish + outputs
 template <int N>
 __device__ __forceinline__ void finish_qp(const mpcqp_params& p, int b, const double* __restrict__ model, Ctx<N>& C,
                                           double x_in, const double z_admm[3], int admm_flag, int admm_it, int nfact,
-                                          double* __restrict__ u0o, double* __restrict__ Xo, double* __restrict__ Uo,
-                                          int32_t* __restrict__ statuso, int32_t* __restrict__ iterso,
-                                          uint8_t* __restrict__ activeo) {
+                                          int pol_it, int n_ls, double* __restrict__ u0o, double* __restrict__ Xo,
+                                          double* __restrict__ Uo, int32_t* __restrict__ statuso,
+                                          int32_t* __restrict__ iterso, uint8_t* __restrict__ activeo) {
   constexpr int n = 2 * N;
   const int lane = threadIdx.x;
   const bool act = C.act;
   const bool use_admm = p.method == MPCQP_METHOD_ADMM;
-  const bool do_polish = !use_admm || p.polish != 0;
+  const bool polished = admm_flag == 2;  // exact optimum already found by an early polish
+  const bool do_polish = (!use_admm || p.polish != 0) && !polished;
   bool bad = admm_flag < 0;  // non-finite data (setup) or ADMM numerical error
-  const bool admm_ok = admm_flag > 0;
+  const bool admm_ok = admm_flag == 1;
   double x = use_admm ? x_in : 0.0;
   const double x_admm = x;
-  bool pol_ok = false;
-  int pol_it = 0, n_ls = 0;
-  Stamps T, T2;
+  bool pol_ok = polished;
+  Stamps T2;
   T2.begin();
-
   if (do_polish && !bad) {
-    double zc[3];
-    int cd[3];
-    C.Cmul(x, zc);
-    // first active-set guess: the ADMM z iterate (the prox output) after an ADMM phase, else the
-    // rows of C x; later guesses classify C x
+    double zg[3];
+    if (use_admm) {  // first guess: the ADMM z iterate (the prox output)
 #pragma unroll
-    for (int r = 0; r < 3; ++r) {
-      const double zg = use_admm ? z_admm[r] : zc[r];
-      cd[r] = zg > C.hi[r] ? 2 : (zg < C.lo[r] ? 1 : 0);
+      for (int r = 0; r < 3; ++r) zg[r] = z_admm[r];
+    } else {
+      C.Cmul(x, zg);
     }
-    constexpr int kMaxRank1 = n / 2;  // more changed rows than this: refactor (form + sweep)
-    double rwf[3] = {0.0, 0.0, 0.0};  // soft-row weights of the current factorization
-    bool have_fact = false;
-    while (pol_it < p.polish_max_iter) {
-      ++pol_it;
-      C.opaque();
-      double rw[3], tmp[3];
-#pragma unroll
-      for (int r = 0; r < 3; ++r) {
-        rw[r] = cd[r] ? 2.0 * C.wb[r] : 0.0;
-        tmp[r] = cd[r] == 2 ? rw[r] * C.hi[r] : (cd[r] == 1 ? rw[r] * C.lo[r] : 0.0);
-      }
-      // Factorize the Newton matrix of this active set: from scratch on the first pass, by
-      // rank-1 updates of the previous inverse when only a few soft rows changed.
-      bool refac = !have_fact;
-      if (!refac) {
-        uint64_t chg[3];
-        int nchg = 0;
-#pragma unroll
-        for (int r = 0; r < 3; ++r) {
-          chg[r] = __ballot(act && rw[r] != rwf[r]);
-          nchg += __popcll(chg[r]);
-        }
-        refac = nchg > kMaxRank1;
-        T.begin();
-#pragma unroll
-        for (int r = 0; r < 3; ++r) {
-          uint64_t m = chg[r];
-          while (m && !refac) {
-            const int l = __builtin_ctzll(m);
-            m &= m - 1;
-            refac = !C.rank1(r, l, readlane(rw[r] - rwf[r], l));
-          }
-        }
-        T.end(1);
-      }
-      if (refac) {
-        T.begin();
-        C.form(0.0, rw);
-        T.end(0);
-        T.begin();
-        const bool okf = C.sweep();
-        T.end(1);
-        if (wave_any(!okf)) {
-          bad = true;
-          break;
-        }
-        have_fact = true;
-      }
-      ++nfact;
-#pragma unroll
-      for (int r = 0; r < 3; ++r) rwf[r] = rw[r];
-      T.begin();
-      const double rhs = C.CTmul(tmp) - C.qv;
-      double xn = C.inv_mul(rhs);
-      {  // one step of iterative refinement: res = rhs - M xn
-        double zz[3], t3[3];
-        C.Cmul(xn, zz);
-#pragma unroll
-        for (int r = 0; r < 3; ++r) t3[r] = rw[r] * zz[r];
-        const double Mx = C.Pmul(xn) + C.CTmul(t3);
-        xn += C.inv_mul(rhs - Mx);
-      }
-      double zn[3];
-      C.Cmul(xn, zn);
-      bool diff = false;
-#pragma unroll
-      for (int r = 0; r < 3; ++r) {
-        const int c2 = zn[r] > C.hi[r] ? 2 : (zn[r] < C.lo[r] ? 1 : 0);
-        diff = diff || (c2 != cd[r]);
-      }
-      T.end(2);
-      if (wave_any(!isfinite(xn))) {
-        bad = true;
-        break;
-      }
-      if (!wave_any(diff)) {
-        x = xn;
-        pol_ok = true;
-        break;
-      }
-      // exact line search along d = xn - x: phi(t) = f(x + t d) is convex piecewise quadratic,
-      // phi' piecewise linear and nondecreasing; semismooth Newton on phi' from t = 1 downwards
-      // lands on the minimizer in [0, 1] after a few pieces (two independent reductions a step)
-      T.begin();
-      const double dx = act ? xn - x : 0.0;
-      const double Px = C.Pmul(x);
-      const double Pd = C.Pmul(dx);
-      double zd[3];
-#pragma unroll
-      for (int r = 0; r < 3; ++r) zd[r] = zn[r] - zc[r];
-      const double qd = wave_sum(act ? dx * Pd : 0.0);
-      const double lin = wave_sum(act ? (Px + C.qv) * dx : 0.0);
-      double t = 1.0;
-      for (int ls = 0; ls < 40; ++ls) {
-        ++n_ls;
-        double g1 = 0.0, g2 = 0.0;
-#pragma unroll
-        for (int r = 0; r < 3; ++r) {
-          const double zt = zc[r] + t * zd[r];
-          const double rr = zt > C.hi[r] ? zt - C.hi[r] : (zt < C.lo[r] ? zt - C.lo[r] : 0.0);
-          g1 += 2.0 * C.wb[r] * rr * zd[r];
-          if (rr != 0.0) g2 += 2.0 * C.wb[r] * zd[r] * zd[r];
-        }
-        const double d1 = lin + t * qd + wave_sum(g1);
-        const double d2 = qd + wave_sum(g2);
-        if (d1 <= 0.0 || !(d2 > 0.0)) break;
-        const double tn = fmax(0.0, t - d1 / d2);
-        if (tn >= t) break;
-        // same linear piece of phi' at tn as at t: tn is that piece's root, the minimizer
-        bool moved = false;
-#pragma unroll
-        for (int r = 0; r < 3; ++r) {
-          const double za = zc[r] + t * zd[r], zb = zc[r] + tn * zd[r];
-          const int ca = za > C.hi[r] ? 2 : (za < C.lo[r] ? 1 : 0);
-          const int cb = zb > C.hi[r] ? 2 : (zb < C.lo[r] ? 1 : 0);
-          moved = moved || ca != cb;
-        }
-        t = tn;
-        if (!wave_any(moved)) break;
-      }
-      x = x + t * dx;
-      C.Cmul(x, zc);
-#pragma unroll
-      for (int r = 0; r < 3; ++r) cd[r] = zc[r] > C.hi[r] ? 2 : (zc[r] < C.lo[r] ? 1 : 0);
-      T.end(3);
-    }
+    const int r_ = polish_qp<N>(C, x, zg, p.polish_max_iter, pol_it, nfact, n_ls);
+    if (r_ < 0) bad = true;
+    pol_ok = r_ > 0;
   }
   T2.end(0);
-  T.flush(8);   // g_stamps[8..11]: polish form, sweep, solve+check, line search
-  T2.flush(12); // g_stamps[12]: polish phase of k_finish
+  T2.flush(12);  // g_stamps[12]: polish phase of k_finish
   if (wave_any(!isfinite(x))) bad = true;
   int status;
   if (bad) {
@@ -822,22 +893,23 @@ __device__ __forceinline__ void finish_qp(const mpcqp_params& p, int b, const do
     status = MPCQP_MAX_ITER_REACHED;
   }
 
-  // ---- outputs (unscaled) ----
+  // ---- outputs (unscaled): speeds W -> accelerations; states by the LTV recursion ----
   const double* mb = model + (size_t)b * model_stride(N);
   const int cc = lane & 1;
-  const double U = act ? C.D * x : 0.0;
+  const double W = act ? C.D * x : 0.0;  // v_{j+1} on lane 2j, delta_j on lane 2j+1
   const double dt = p.dt;
   const double x00 = mb[11 * N + 4], x01 = mb[11 * N + 5], x02 = mb[11 * N + 6], x03 = mb[11 * N + 7];
   const double up0 = mb[11 * N + 8], up1 = mb[11 * N + 9];
+  const double Wm2 = shr2(W);
+  const double U = !act ? 0.0 : (cc == 1 ? W : (W - (lane == 0 ? x03 : Wm2)) / dt);
   const double sj = act ? mb[4 * N + (lane >> 1)] : 0.0;
-  // v_{j+1} on lane 2j, psi_{j+1} on lane 2j+1
-  const double vacc = scan_add(C.even ? U : 0.0, lane);
+  // psi_{j+1} on lane 2j+1
   const double sacc = scan_add((act && cc == 1) ? sj * U : 0.0, lane);
   // lane k <- (psi_k, v_k)
   const int srcv = lane == 0 ? 0 : 2 * (lane - 1);
-  const double vk_s = __shfl(vacc, srcv < kWave ? srcv : 0, kWave);
+  const double vk_s = __shfl(W, srcv < kWave ? srcv : 0, kWave);
   const double pk_s = __shfl(sacc, (srcv + 1) < kWave ? srcv + 1 : 0, kWave);
-  const double vk = lane == 0 ? x03 : x03 + dt * vk_s;
+  const double vk = lane == 0 ? x03 : vk_s;
   const double pk = lane == 0 ? x02 : x02 + pk_s;
   double t0 = 0.0, t1 = 0.0;
   if (lane < N) {
@@ -900,9 +972,9 @@ __global__ __launch_bounds__(kWave) void k_solve(mpcqp_params p, int B, const ui
   Ctx<N> C;
   const bool bad = setup_qp<N>(p, b, model, C, sm, state + (size_t)b * state_stride(N), dbg);
   double x = 0.0, z[3] = {0.0, 0.0, 0.0};
-  int flag = bad ? -1 : 0, it = 0, nfact = 0;
-  if (p.method == MPCQP_METHOD_ADMM) flag = admm_qp<N>(p, C, bad, x, z, it, nfact, dbg);
-  finish_qp<N>(p, b, model, C, x, z, flag, it, nfact, u0o, Xo, Uo, statuso, iterso, activeo);
+  int flag = bad ? -1 : 0, it = 0, nfact = 0, pol_it = 0, n_ls = 0;
+  if (p.method == MPCQP_METHOD_ADMM) flag = admm_qp<N>(p, C, bad, x, z, it, nfact, pol_it, n_ls, dbg);
+  finish_qp<N>(p, b, model, C, x, z, flag, it, nfact, pol_it, n_ls, u0o, Xo, Uo, statuso, iterso, activeo);
   if (dbg && threadIdx.x == 0)  // this wave's cycles, start to finish (tools/qp_cycles.py)
     dbg[state_scal_off(N) + 4] = (double)(__builtin_amdgcn_s_memtime() - t_start);
 }

@@ -33,6 +33,8 @@ STATUS_NAMES = {
 
 # OSQP settings used by the reference (src/control/mpc_controller.py:121-131) plus the
 # OSQP defaults it relies on implicitly.
+ABI_VERSION = 2  # MPCQP_ABI_VERSION (include/mpcqp.h)
+
 DEFAULT_SOLVER_SETTINGS = dict(
     rho=0.1,
     sigma=1e-6,
@@ -48,6 +50,8 @@ DEFAULT_SOLVER_SETTINGS = dict(
     polish=1,
     polish_max_iter=100,
     debug_state=0,
+    polish_from=150,
+    polish_attempt_max_iter=30,
 )
 
 
@@ -82,6 +86,8 @@ class MpcqpParams(ctypes.Structure):
         ("polish", ctypes.c_int32),
         ("polish_max_iter", ctypes.c_int32),
         ("debug_state", ctypes.c_int32),
+        ("polish_from", ctypes.c_int32),
+        ("polish_attempt_max_iter", ctypes.c_int32),
     ]
 
 
@@ -214,8 +220,9 @@ def lib() -> ctypes.CDLL:
         fn = getattr(handle, name)
         fn.argtypes = argtypes
         fn.restype = restype
-    if handle.mpcqp_version() != 1:
-        raise LibraryError("libmpcqp ABI version mismatch")
+    # MPCQP_ABI_ANY: development A/B runs against an older kernel build (tools/diag)
+    if handle.mpcqp_version() != ABI_VERSION and not os.environ.get("MPCQP_ABI_ANY"):
+        raise LibraryError(f"libmpcqp ABI version {handle.mpcqp_version()} != {ABI_VERSION}")
     _lib = handle
     return handle
 

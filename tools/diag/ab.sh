@@ -6,7 +6,7 @@ for lib in tools/diag/libmpcqp_*.so; do
   v=$(basename $lib .so); v=${v#libmpcqp_}
   [ "$v" = stamps ] && continue
   for B in 512 4096; do
-    MPCQP_LIB=$lib timeout -k 10 120 python bench.py --batch $B --steps 20 --warmup 3 --cpu-seconds 0 > gpurun_out/ab_${v}_$B.json || exit 1
+    MPCQP_ABI_ANY=1 MPCQP_LIB=$lib timeout -k 10 120 python bench.py --batch $B --steps 20 --warmup 3 --cpu-seconds 0 > gpurun_out/ab_${v}_$B.json || exit 1
     python -c "import json; d=json.load(open('gpurun_out/ab_${v}_$B.json')); print('$v', $B, round(d['value']), round(d['kernel_ms']['k_solve'],4), d['solved_fraction'])"
   done
 done
