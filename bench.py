@@ -154,6 +154,8 @@ def main() -> int:
     ap.add_argument("--config", default="config3", choices=["config2", "config3", "config4"])
     ap.add_argument("--batch", type=int, default=0, help="QPs per GPU (default: the config's)")
     ap.add_argument("--method", default="admm", choices=["admm", "newton"])
+    ap.add_argument("--polish-from", type=int, default=None,
+                    help="ADMM iteration of the first early polish attempt (default: the library's; 0 = off)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline sample length (0 = skip)")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="torch.distributed backend for N > 1 (nccl = RCCL; gloo only to rehearse "
@@ -186,7 +188,8 @@ def main() -> int:
     B = args.batch or default_batch
     x0, ref, u_prev, N, name = make_batch(args.config, B, world, rank)
     params = MPCConfig(horizon=N).to_parameters(0.8)
-    ctrl = BatchedMPCController(params, B, device=device, method=args.method)
+    extra = {} if args.polish_from is None else {"polish_from": args.polish_from}
+    ctrl = BatchedMPCController(params, B, device=device, method=args.method, **extra)
     x0_t = torch.from_numpy(x0).to(device)
     ref_t = torch.from_numpy(ref).to(device)
     up_t = torch.from_numpy(u_prev).to(device)

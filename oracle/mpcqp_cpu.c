@@ -489,15 +489,16 @@ void mpcqp_cpu_state(const mpcqp_params* p, const double* model, double* out) {
 /* ---------------------------------------------------------------- polish */
 /* Semismooth Newton / active-set iteration on the scaled problem from x (in/out): the first
    active-set guess classifies zg, later ones C x.  Each pass solves the Newton system of the
-   current set (with one step of iterative refinement); a set that reproduces itself is the
-   exact optimum (returns 1, x = that optimum); otherwise an exact line search along the Newton
-   step.  0: not found within max_it passes (x = the last iterate), -1: numerical failure. */
+   current set; a set that reproduces itself (checked again after one step of iterative
+   refinement) is the exact optimum (returns 1, x = that optimum); otherwise an exact line
+   search along the Newton step.  0: not found within max_it passes (x = the last iterate), -1: numerical failure. */
 static int polish_run(qp_t* s, double* x, const double* zg, int max_it, int* pol_it, int* n_fact, int* n_ls) {
   const int n = s->n, m = s->m;
   uint8_t cd[MAXR], cn[MAXR];
   double zc[MAXR], rw[MAXR], tmp[MAXR], rhs[MAXNV], xn[MAXNV], res[MAXNV], dx[MAXNV], Px[MAXNV], Pd[MAXNV], zd[MAXR],
       zn[MAXR];
   Cmul(s, x, zc);
+  matvec(n, s->P, x, Px); /* P x, carried along the passes */
   codes_of(s, zg, cd);
   for (int it = 1; it <= max_it; ++it) {
     ++*pol_it;
@@ -512,26 +513,37 @@ static int polish_run(qp_t* s, double* x, const double* zg, int max_it, int* pol
     CTmul(s, tmp, rhs);
     for (int i = 0; i < n; ++i) rhs[i] -= s->q[i];
     matvec(n, s->K, rhs, xn);
-    /* one step of iterative refinement */
-    matvec(n, s->M, xn, res);
-    for (int i = 0; i < n; ++i) res[i] = rhs[i] - res[i];
-    matvec(n, s->K, res, dx);
-    for (int i = 0; i < n; ++i) xn[i] += dx[i];
     Cmul(s, xn, zn);
     codes_of(s, zn, cn);
     int nonfinite = 0;
     for (int i = 0; i < n; ++i) nonfinite |= !isfinite(xn[i]);
     if (nonfinite) return -1;
     if (memcmp(cn, cd, m) == 0) {
-      memcpy(x, xn, sizeof(double) * n);
-      return 1;
+      /* the set reproduces itself: one step of iterative refinement, then accept if it still does */
+      matvec(n, s->M, xn, res);
+      for (int i = 0; i < n; ++i) res[i] = rhs[i] - res[i];
+      matvec(n, s->K, res, dx);
+      for (int i = 0; i < n; ++i) xn[i] += dx[i];
+      Cmul(s, xn, zn);
+      codes_of(s, zn, cn);
+      nonfinite = 0;
+      for (int i = 0; i < n; ++i) nonfinite |= !isfinite(xn[i]);
+      if (nonfinite) return -1;
+      if (memcmp(cn, cd, m) == 0) {
+        memcpy(x, xn, sizeof(double) * n);
+        return 1;
+      }
     }
     /* exact line search along d = xn - x: phi(t) = f(x + t d) is convex piecewise quadratic, its
        derivative piecewise linear and nondecreasing; semismooth Newton on phi' from t = 1
-       downwards reaches the minimizer in [0, 1] in a few pieces */
-    for (int i = 0; i < n; ++i) dx[i] = xn[i] - x[i];
-    matvec(n, s->P, x, Px);
-    matvec(n, s->P, dx, Pd);
+       downwards reaches the minimizer in [0, 1] in a few pieces.  P xn from the Newton system
+       (P xn + q = -C' rw (C xn - bound)), so no product with P. */
+    for (int r = 0; r < m; ++r) tmp[r] = rw[r] * (zn[r] - (cd[r] == 2 ? s->u[r] : (cd[r] == 1 ? s->l[r] : 0.0)));
+    CTmul(s, tmp, Pd);
+    for (int i = 0; i < n; ++i) {
+      dx[i] = xn[i] - x[i];
+      Pd[i] = (-Pd[i] - s->q[i]) - Px[i];
+    }
     for (int r = 0; r < m; ++r) zd[r] = zn[r] - zc[r];
     double qd = 0.0, lin = 0.0;
     for (int i = 0; i < n; ++i) {
@@ -562,7 +574,10 @@ static int polish_run(qp_t* s, double* x, const double* zg, int max_it, int* pol
       t = tn;
       if (same) break;
     }
-    for (int i = 0; i < n; ++i) x[i] += t * dx[i];
+    for (int i = 0; i < n; ++i) {
+      x[i] += t * dx[i];
+      Px[i] += t * Pd[i];
+    }
     Cmul(s, x, zc);
     codes_of(s, zc, cd);
   }

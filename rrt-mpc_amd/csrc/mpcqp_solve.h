@@ -548,6 +548,7 @@ __device__ __forceinline__ int polish_qp(Ctx<N>& C, double& x, const double zg[3
   double zc[3];
   int cd[3];
   C.Cmul(x, zc);
+  double Px = C.Pmul(x);  // P x, carried along the passes
 #pragma unroll
   for (int r = 0; r < 3; ++r) cd[r] = zg[r] > C.hi[r] ? 2 : (zg[r] < C.lo[r] ? 1 : 0);
   constexpr int kMaxRank1 = n / 2;  // more changed rows than this: refactor (form + sweep)
@@ -605,14 +606,6 @@ __device__ __forceinline__ int polish_qp(Ctx<N>& C, double& x, const double zg[3
     T.begin();
     const double rhs = C.CTmul(tmp) - C.qv;
     double xn = C.inv_mul(rhs);
-    {  // one step of iterative refinement: res = rhs - M xn
-      double zz[3], t3[3];
-      C.Cmul(xn, zz);
-#pragma unroll
-      for (int r = 0; r < 3; ++r) t3[r] = rw[r] * zz[r];
-      const double Mx = C.Pmul(xn) + C.CTmul(t3);
-      xn += C.inv_mul(rhs - Mx);
-    }
     double zn[3];
     C.Cmul(xn, zn);
     bool diff = false;
@@ -621,23 +614,50 @@ __device__ __forceinline__ int polish_qp(Ctx<N>& C, double& x, const double zg[3
       const int c2 = zn[r] > C.hi[r] ? 2 : (zn[r] < C.lo[r] ? 1 : 0);
       diff = diff || (c2 != cd[r]);
     }
-    T.end(2);
     if (wave_any(!isfinite(xn))) {
+      T.end(2);
       result = -1;
       break;
     }
     if (!wave_any(diff)) {
-      x = xn;
-      result = 1;
-      break;
+      // the set reproduces itself: one step of iterative refinement (res = rhs - M xn), then
+      // accept if it still does
+      double t3[3];
+#pragma unroll
+      for (int r = 0; r < 3; ++r) t3[r] = rw[r] * zn[r];
+      const double Mx = C.Pmul(xn) + C.CTmul(t3);
+      xn += C.inv_mul(rhs - Mx);
+      C.Cmul(xn, zn);
+      diff = false;
+#pragma unroll
+      for (int r = 0; r < 3; ++r) {
+        const int c2 = zn[r] > C.hi[r] ? 2 : (zn[r] < C.lo[r] ? 1 : 0);
+        diff = diff || (c2 != cd[r]);
+      }
+      if (wave_any(!isfinite(xn))) {
+        T.end(2);
+        result = -1;
+        break;
+      }
+      if (!wave_any(diff)) {
+        T.end(2);
+        x = xn;
+        result = 1;
+        break;
+      }
     }
+    T.end(2);
     // exact line search along d = xn - x: phi(t) = f(x + t d) is convex piecewise quadratic,
     // phi' piecewise linear and nondecreasing; semismooth Newton on phi' from t = 1 downwards
-    // lands on the minimizer in [0, 1] after a few pieces (two independent reductions a step)
+    // lands on the minimizer in [0, 1] after a few pieces (two independent reductions a step).
+    // P xn from the Newton system (P xn + q = -C' rw (C xn - bound)): no product with P.
     T.begin();
+    double tb[3];
+#pragma unroll
+    for (int r = 0; r < 3; ++r)
+      tb[r] = rw[r] * (zn[r] - (cd[r] == 2 ? C.hi[r] : (cd[r] == 1 ? C.lo[r] : 0.0)));
     const double dx = act ? xn - x : 0.0;
-    const double Px = C.Pmul(x);
-    const double Pd = C.Pmul(dx);
+    const double Pd = act ? (-C.CTmul(tb) - C.qv) - Px : 0.0;
     double zd[3];
 #pragma unroll
     for (int r = 0; r < 3; ++r) zd[r] = zn[r] - zc[r];
@@ -672,6 +692,7 @@ __device__ __forceinline__ int polish_qp(Ctx<N>& C, double& x, const double zg[3
       if (!wave_any(moved)) break;
     }
     x = x + t * dx;
+    Px = Px + t * Pd;
     C.Cmul(x, zc);
 #pragma unroll
     for (int r = 0; r < 3; ++r) cd[r] = zc[r] > C.hi[r] ? 2 : (zc[r] < C.lo[r] ? 1 : 0);
