@@ -167,14 +167,19 @@ struct Ctx {
   // kappa = delta / (1 + delta c'u).  Used by the polish when a few soft rows enter or leave
   // the active set.  false (inverse untouched) when 1 + delta c'u is not safely positive.
   __device__ __forceinline__ bool rank1(int tau, int l, double delta) {
-    // the row's coefficients on the variables l, l-2, l-4 (lane l's e)
-    const double c0 = readlane(tau == 0 ? E[0] : (tau == 1 ? e1[0] : e2[0]), l);
-    const double c1 = readlane(tau == 1 ? e1[1] : (tau == 2 ? e2[1] : 0.0), l);
-    const double c2 = readlane(tau == 2 ? e2[2] : 0.0, l);
-    double c = lane == l ? c0 : (lane + 2 == l ? c1 : (lane + 4 == l ? c2 : 0.0));
-    c = act ? c * D : 0.0;
-    const double u = inv_mul(c);
-    const double den = 1.0 + delta * wave_sum(c * u);
+    const int lu = __builtin_amdgcn_readfirstlane(l);
+    // the row's coefficients on the variables lu, lu-2, lu-4 (lane lu's e, times D there)
+    const double c0 = readlane(tau == 0 ? E[0] : (tau == 1 ? e1[0] : e2[0]), lu) * readlane(D, lu);
+    const double c1 = lu >= 2 ? readlane(tau == 1 ? e1[1] : (tau == 2 ? e2[1] : 0.0), lu) * readlane(D, lu - 2) : 0.0;
+    const double c2 = lu >= 4 ? readlane(tau == 2 ? e2[2] : 0.0, lu) * readlane(D, lu - 4) : 0.0;
+    // u = A^{-1} c: c has at most three entries, so u is three columns of the inverse -- by
+    // symmetry the lane's own registers r[lu], r[lu-2], r[lu-4] (A^{-1}[i][j] = -r_i[j])
+    double u = c0 * pick<0, n>(lu);
+    if (lu >= 2) u += c1 * pick<0, n>(lu - 2);
+    if (lu >= 4) u += c2 * pick<0, n>(lu - 4);
+    u = act ? -u : 0.0;
+    const double cu = (c0 * readlane(u, lu) + c1 * readlane(u, lu >= 2 ? lu - 2 : 0)) + c2 * readlane(u, lu >= 4 ? lu - 4 : 0);
+    const double den = 1.0 + delta * cu;
     if (!(den > kRank1Min) || !isfinite(den)) return false;
     const double m = (delta / den) * u;
     double w[4];
@@ -184,6 +189,18 @@ struct Ctx {
       fmac_bc<j % 16>(r[j], w[j / 16], m);
     });
     return true;
+  }
+  // r[j] of this lane for a wave-uniform j: a scalar branch tree (log2 n uniform branches), no
+  // per-lane selects
+  template <int LO, int HI>
+  __device__ __forceinline__ double pick(int j) const {
+    if constexpr (HI - LO == 1) {
+      return r[LO];
+    } else {
+      constexpr int M = (LO + HI) / 2;
+      if (j < M) return pick<LO, M>(j);
+      return pick<M, HI>(j);
+    }
   }
   // (A^{-1} v)_lane
   __device__ __forceinline__ double inv_mul(double v) const {
