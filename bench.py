@@ -39,16 +39,21 @@ def qp_bytes(N: int) -> int:
 
 
 def qp_flops(N: int, iters: np.ndarray, scaling: int = 10, check: int = 25) -> np.ndarray:
-    """Algorithmic FP64 flops per QP as implemented:
-    condensing + Ruiz + KKT factorizations (explicit SPD inverse: n^3) + ADMM iterations
-    (dense n x n inverse product + structured row operators) + polish iterations
-    (2 inverse products, refinement and line-search P products) + line-search trials."""
+    """Algorithmic FP64 flops per QP as implemented, from the kernel's counters
+    (ADMM iterations, polish passes, factorizations + passes, line-search trials):
+      setup      condensing 50 N (n+1) + Ruiz `scaling` x 3 n^2
+      ADMM       (factorizations - passes) x (n^3 + 4 n^2): explicit SPD inverse by the sweep;
+                 iterations x (2 n^2 + 30 n): dense inverse product + banded row operators + prox;
+                 one termination check per `check` iterations x (2 n^2 + 30 n)
+      polish     one full factorization per polish run, then per pass 2 n^2 (inverse product)
+                 + 2 n^2 (one rank-1 update of the inverse, a floor: a pass updates every changed
+                 row) + 40 n; 4 n^2 for the final refinement; line-search trials x 10 m."""
     n, m = 2 * N, 5 * N
     admm, pol, fact, ls = (iters[:, i].astype(np.float64) for i in range(4))
     f = 50.0 * N * (n + 1) + scaling * 3.0 * n * n
-    f = f + fact * (n ** 3 + 4.0 * n * n)
-    f = f + admm * (2.0 * n * n + 45.0 * n) + np.floor(admm / check) * (2.0 * n * n + 30.0 * n)
-    f = f + pol * (8.0 * n * n + 60.0 * n)
+    f = f + np.maximum(fact - pol, 0.0) * (n ** 3 + 4.0 * n * n)
+    f = f + admm * (2.0 * n * n + 30.0 * n) + np.floor(admm / check) * (2.0 * n * n + 30.0 * n)
+    f = f + (pol > 0) * (n ** 3 + 4.0 * n * n + 4.0 * n * n) + pol * (4.0 * n * n + 40.0 * n)
     f = f + ls * (10.0 * m)
     return f
 
