@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define MPCQP_ABI_VERSION 2
+#define MPCQP_ABI_VERSION 3
 
 /* error codes (function return values) */
 #define MPCQP_OK 0
@@ -100,6 +100,8 @@ typedef struct mpcqp_params {
                                  self-consistent active set is the exact optimum and ends the solve as
                                  solved, a failed attempt resumes ADMM.  0: polish only after ADMM stops */
   int32_t polish_attempt_max_iter; /* 30 */
+  double polish_near;         /* 3: also attempt the polish from iteration 2*check_termination on when
+                                 both residuals are within this factor of their tolerances; 0 off */
 } mpcqp_params;
 
 typedef struct mpcqp_ws mpcqp_ws;

@@ -695,7 +695,10 @@ void mpcqp_cpu_solve_one(const mpcqp_params* p, const double* model, double* u0,
           break;
         }
         /* early polish: an exact optimum found now satisfies the termination test itself */
-        if (p->polish && p->polish_from > 0 && it >= p->polish_from && it < p->max_iter) {
+        /* ... from polish_from on, or earlier once both residuals are near their tolerances */
+        const int near = p->polish_near > 0.0 && it >= 2 * p->check_termination &&
+                         fmax(pr / ep, du / ed) < p->polish_near;
+        if (p->polish && p->polish_from > 0 && (it >= p->polish_from || near) && it < p->max_iter) {
           memcpy(xp, x, sizeof(double) * n);
           const int pr_ = polish_run(s, xp, z, p->polish_attempt_max_iter, &pol_it, &n_fact, &n_ls);
           if (pr_ < 0) {

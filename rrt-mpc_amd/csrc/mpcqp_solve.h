@@ -836,7 +836,10 @@ __device__ __forceinline__ int admm_qp(const mpcqp_params& p, Ctx<N>& C, bool ba
           ok = true;
           break;
         }
-        if (early && it >= p.polish_from && it < p.max_iter) {
+        // ... from polish_from on, or earlier once both residuals are near their tolerances
+        const bool near = p.polish_near > 0.0 && it >= 2 * p.check_termination &&
+                          fmax(pr / ep, du / ed) < p.polish_near;
+        if (early && (it >= p.polish_from || near) && it < p.max_iter) {
           double xp = x;
           const int pr_ = polish_qp<N>(C, xp, z, p.polish_attempt_max_iter, pol_it, nfact, n_ls);
           if (pr_ < 0) {

@@ -33,7 +33,7 @@ STATUS_NAMES = {
 
 # OSQP settings used by the reference (src/control/mpc_controller.py:121-131) plus the
 # OSQP defaults it relies on implicitly.
-ABI_VERSION = 2  # MPCQP_ABI_VERSION (include/mpcqp.h)
+ABI_VERSION = 3  # MPCQP_ABI_VERSION (include/mpcqp.h)
 
 DEFAULT_SOLVER_SETTINGS = dict(
     rho=0.1,
@@ -52,6 +52,7 @@ DEFAULT_SOLVER_SETTINGS = dict(
     debug_state=0,
     polish_from=150,
     polish_attempt_max_iter=30,
+    polish_near=3.0,
 )
 
 
@@ -88,6 +89,7 @@ class MpcqpParams(ctypes.Structure):
         ("debug_state", ctypes.c_int32),
         ("polish_from", ctypes.c_int32),
         ("polish_attempt_max_iter", ctypes.c_int32),
+        ("polish_near", ctypes.c_double),
     ]
 
 
