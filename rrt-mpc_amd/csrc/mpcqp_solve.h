@@ -995,12 +995,14 @@ __device__ __forceinline__ void finish_qp(const mpcqp_params& p, int b, const do
 // the batch drains once (the slowest QP's whole chain) instead of once per phase.  The scaled
 // problem never leaves the CU: Pbar stays in LDS, the per-lane data and the KKT inverse in
 // registers (the state buffer is written only when debug_state is set).
-// Occupancy: ~180 VGPRs (the KKT inverse is 2n of them) give 2 waves per SIMD.  Capping the
+// Occupancy: ~225 VGPRs (the KKT inverse is 2n of them) give 2 waves per SIMD; the launch
+// bound's 2 keeps the compiler from trading that for AGPR spills (a branch-free condensing
+// variant did, and ran at 1 wave per SIMD, +35 % at B = 4096).  Capping the
 // registers for a third wave (168, fits the ~13 KB of LDS at N = 20) measured no faster at
 // B = 4096: the four QPs per SIMD then run in 1.33 rounds instead of 2, but each wave shares
 // its SIMD's FP64 issue with two others.
 template <int N>
-__global__ __launch_bounds__(kWave) void k_solve(mpcqp_params p, int B, const uint8_t* __restrict__ mask,
+__global__ __launch_bounds__(kWave, 2) void k_solve(mpcqp_params p, int B, const uint8_t* __restrict__ mask,
                                                  const double* __restrict__ model, double* __restrict__ state,
                                                  double* __restrict__ u0o, double* __restrict__ Xo,
                                                  double* __restrict__ Uo, int32_t* __restrict__ statuso,
