@@ -47,7 +47,6 @@ struct Ctx {
   double cscale;
   const double* __restrict__ P;  // Pbar (LDS, row-major n x n)
   static constexpr int kNW = (n + 15) / 16;  // 16-lane rows holding the n variables
-  static constexpr int kPickMaxN = 48;         // rank-1 columns by register pick up to this n
   // KKT inverse, row `lane`: A^{-1}[lane][j] = -r[j] (symmetric sweep operator)
   double r[n];
 
@@ -175,16 +174,10 @@ struct Ctx {
     const double c2 = lu >= 4 ? readlane(tau == 2 ? e2[2] : 0.0, lu) * readlane(D, lu - 4) : 0.0;
     // u = A^{-1} c: c has at most three entries, so u is three columns of the inverse -- by
     // symmetry the lane's own registers r[lu], r[lu-2], r[lu-4] (A^{-1}[i][j] = -r_i[j])
-    double u;
-    if constexpr (n <= kPickMaxN) {
-      u = c0 * pick<0, n>(lu);
-      if (lu >= 2) u += c1 * pick<0, n>(lu - 2);
-      if (lu >= 4) u += c2 * pick<0, n>(lu - 4);
-      u = act ? -u : 0.0;
-    } else {  // long horizons: the branch tree would push the inverse row out to scratch
-      const double cv = lane == lu ? c0 : (lane + 2 == lu ? c1 : (lane + 4 == lu ? c2 : 0.0));
-      u = inv_mul(act ? cv : 0.0);
-    }
+    double u = c0 * pick<0, n>(lu);
+    if (lu >= 2) u += c1 * pick<0, n>(lu - 2);
+    if (lu >= 4) u += c2 * pick<0, n>(lu - 4);
+    u = act ? -u : 0.0;
     const double cu = (c0 * readlane(u, lu) + c1 * readlane(u, lu >= 2 ? lu - 2 : 0)) + c2 * readlane(u, lu >= 4 ? lu - 4 : 0);
     const double den = 1.0 + delta * cu;
     if (!(den > kRank1Min) || !isfinite(den)) return false;
@@ -197,12 +190,16 @@ struct Ctx {
     });
     return true;
   }
-  // r[j] of this lane for a wave-uniform j: a scalar branch tree (log2 n uniform branches), no
-  // per-lane selects
+  // r[j] of this lane for a wave-uniform j: uniform branches down to pairs of registers, one
+  // select in the pair.  The asm pins each pair's value: merged through a phi as one load of a
+  // variable address, the inverse row would be demoted to scratch memory.
   template <int LO, int HI>
   __device__ __forceinline__ double pick(int j) const {
-    if constexpr (HI - LO == 1) {
-      return r[LO];
+    if constexpr (HI - LO <= 2) {
+      double v = r[LO];
+      if constexpr (HI - LO == 2) v = j == LO + 1 ? r[LO + 1] : v;
+      asm volatile("" : "+v"(v));
+      return v;
     } else {
       constexpr int M = (LO + HI) / 2;
       if (j < M) return pick<LO, M>(j);

@@ -201,3 +201,19 @@ def test_window_gather_matches_reference_loop(golden):
     for k, w in enumerate(wins):
         idx = int(np.argmin(np.abs(ref_g[:, 0] - w[0, 0]) + np.abs(ref_g[:, 1] - w[0, 1])))
         np.testing.assert_array_equal(window_at(ref_g, idx, 15), w)
+
+
+def test_solver_kernel_resources():
+    """Every k_solve<N> keeps 2 waves per SIMD and its working set in registers: the build
+    records hipcc's resource remarks (build/kernel_resources.json).  A demoted KKT-inverse
+    row (scratch memory) once made config 4 (N = 30) 25x slower."""
+    import json
+
+    path = ROOT / "build" / "kernel_resources.json"
+    if not path.exists():
+        pytest.skip("library not built in this tree (build() writes the resource record)")
+    res = {int(k): v for k, v in json.loads(path.read_text()).items()}
+    assert sorted(res) == list(range(1, 32))
+    for N, r in res.items():
+        assert r["Occupancy"] >= 2 and r["AGPRs"] == 0, (N, r)
+        assert r["ScratchSize"] <= (0 if N <= 29 else 64), (N, r)
