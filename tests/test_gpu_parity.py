@@ -75,15 +75,22 @@ def test_newton_method_matches(cuda):
     _check_against_oracle(params, batch.x0, batch.ref, batch.u_prev, out, range(0, 256, 5))
 
 
-def test_iteration_counts_match_cpu_restatement(cuda):
-    """ADMM / polish iteration counts of the GPU against the C restatement (same algorithm)."""
+@pytest.mark.parametrize("schedule", [
+    {},                                       # the default polish schedule (early + near-tolerance)
+    {"polish_near": 0.0},                     # early polish from iteration 150 only
+    {"polish_from": 0, "polish_near": 0.0},   # OSQP's order: polish only after ADMM stops
+])
+def test_iteration_counts_match_cpu_restatement(cuda, schedule):
+    """ADMM / polish iteration counts of the GPU against the C restatement (same algorithm),
+    under each polish schedule; the solutions are the exact optimum in every case."""
     import cpu_solver
     from mpcqp import scenarios
 
     batch = scenarios.config3(512)
     params = _params(20)
-    out = _solve(params, batch.x0, batch.ref, batch.u_prev)
-    ref = cpu_solver.cpu_solve(params, batch.x0, batch.ref, batch.u_prev)
+    out = _solve(params, batch.x0, batch.ref, batch.u_prev, **schedule)
+    ref = cpu_solver.cpu_solve(params, batch.x0, batch.ref, batch.u_prev, **schedule)
+    assert (out["status"] == 1).all()
     same = (out["iters"] == ref["iters"]).all(axis=1)
     # rounding differs (wavefront tree reductions vs sequential sums); the iteration
     # counts must agree for the overwhelming majority and the solutions for all
