@@ -161,6 +161,10 @@ def main() -> int:
     ap.add_argument("--method", default="admm", choices=["admm", "newton"])
     ap.add_argument("--polish-from", type=int, default=None,
                     help="ADMM iteration of the first early polish attempt (default: the library's; 0 = off)")
+    ap.add_argument("--polish-near", type=float, default=None,
+                    help="residual/tolerance ratio that triggers an early polish (default: the library's; 0 = off)")
+    ap.add_argument("--set", action="append", default=[], metavar="KEY=VALUE",
+                    help="development: override a solver setting of mpcqp_params (repeatable)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline sample length (0 = skip)")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="torch.distributed backend for N > 1 (nccl = RCCL; gloo only to rehearse "
@@ -194,6 +198,11 @@ def main() -> int:
     x0, ref, u_prev, N, name = make_batch(args.config, B, world, rank)
     params = MPCConfig(horizon=N).to_parameters(0.8)
     extra = {} if args.polish_from is None else {"polish_from": args.polish_from}
+    if args.polish_near is not None:
+        extra["polish_near"] = args.polish_near
+    for kv in args.set:
+        k, v = kv.split("=", 1)
+        extra[k] = float(v) if "." in v or "e" in v else int(v)
     ctrl = BatchedMPCController(params, B, device=device, method=args.method, **extra)
     x0_t = torch.from_numpy(x0).to(device)
     ref_t = torch.from_numpy(ref).to(device)
