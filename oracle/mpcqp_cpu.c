@@ -406,11 +406,13 @@ static void setup_qp(const mpcqp_params* p, const double* model, qp_t* s) {
   for (int i = 0; i < n; ++i) s->D[i] = 1.0;
   for (int r = 0; r < m; ++r) s->E[r] = 1.0;
   s->c = 1.0;
+  double cpend = 1.0; /* cost factor not yet applied to P */
   for (int it = 0; it < p->scaling; ++it) {
     double dl[MAXNV], el[MAXR];
     for (int q = 0; q < n; ++q) {
       double cp = 0.0;
       for (int i = 0; i < n; ++i) cp = fmax(cp, fabs(s->P[i][q]));
+      cp *= cpend; /* the stored P still lacks the last cost factor */
       /* column q of Cbar: its own v / input / rate rows, the rows 2 and 4 ahead */
       double cc = (q & 1) == 0 ? s->E[q / 2] : 0.0;
       cc = fmax(cc, s->E[N + q] * fabs(s->k1[q][0]));
@@ -431,10 +433,14 @@ static void setup_qp(const mpcqp_params* p, const double* model, qp_t* s) {
       el[N + q] = 1.0 / sqrt(limit_scaling(s->E[N + q] * r1));
       el[3 * N + q] = 1.0 / sqrt(limit_scaling(s->E[3 * N + q] * r2));
     }
+    /* the previous pass's cost factor is folded into this pass's column scaling (as k_solve) */
+    for (int j = 0; j < n; ++j) {
+      const double dlc = dl[j] * cpend;
+      for (int i = 0; i < n; ++i) s->P[i][j] = s->P[i][j] * (dl[i] * dlc);
+    }
     for (int i = 0; i < n; ++i) {
       s->D[i] *= dl[i];
       s->q[i] *= dl[i];
-      for (int j = 0; j < n; ++j) s->P[i][j] *= dl[i] * dl[j];
     }
     for (int r = 0; r < m; ++r) s->E[r] *= el[r];
     double cn = 0.0;
@@ -445,12 +451,12 @@ static void setup_qp(const mpcqp_params* p, const double* model, qp_t* s) {
     }
     cn /= n;
     double ct = 1.0 / limit_scaling(fmax(cn, limit_scaling(vmaxabs(n, s->q))));
-    for (int i = 0; i < n; ++i) {
-      s->q[i] *= ct;
-      for (int j = 0; j < n; ++j) s->P[i][j] *= ct;
-    }
+    cpend = ct;
+    for (int i = 0; i < n; ++i) s->q[i] *= ct;
     s->c *= ct;
   }
+  for (int i = 0; i < n; ++i)
+    for (int j = 0; j < n; ++j) s->P[i][j] *= cpend;
   for (int r = 0; r < m; ++r) {
     s->l[r] = s->E[r] * lo0[r];
     s->u[r] = s->E[r] * hi0[r];

@@ -435,6 +435,14 @@ __device__ __forceinline__ bool setup_qp(const mpcqp_params& p, int b, const dou
   T.begin();
 
   // ---- Ruiz equilibration + cost scaling (OSQP scale_data, `scaling` iterations) ----
+  // 1/sqrt by v_rsq_f64 + two Newton steps (within an ulp; any positive scaling is a valid
+  // equilibration), the cost factor of each pass folded into the next pass's column scaling
+  auto rsqrt = [](double v) {
+    double y = __builtin_amdgcn_rsq(v);
+    y = y * fma(-0.5 * v, y * y, 1.5);
+    return y * fma(-0.5 * v, y * y, 1.5);
+  };
+  double cpend = 1.0;  // cost factor not yet applied to Pc
   for (int it = 0; it < p.scaling; ++it) {
     // column norms of [P; A] (first n columns of the KKT matrix): the lane's own rows and
     // the banded rows 2 and 4 ahead
@@ -442,22 +450,23 @@ __device__ __forceinline__ bool setup_qp(const mpcqp_params& p, int b, const dou
     ccol = fmax(ccol, shl2(fmax(E[1] * fabs(k1[1]), E[2] * fabs(k2[1]))));
     ccol = fmax(ccol, shl4(E[2] * fabs(k2[2])));
     ccol *= D;
-    const double dl = act ? 1.0 / sqrt(limit_scaling(fmax(cmax, ccol))) : 0.0;
+    const double dl = act ? rsqrt(limit_scaling(fmax(cmax, ccol))) : 0.0;
     // row norms of A
     const double Dm2 = shr2(D), Dm4 = shr2(Dm2);
     const double r1 = fmax(fabs(k1[0]) * D, fabs(k1[1]) * Dm2);
     const double r2 = fmax(fmax(fabs(k2[0]) * D, fabs(k2[1]) * Dm2), fabs(k2[2]) * Dm4);
-    const double el0 = even ? 1.0 / sqrt(limit_scaling(E[0] * D)) : 0.0;
-    const double el1 = act ? 1.0 / sqrt(limit_scaling(E[1] * r1)) : 0.0;
-    const double el2 = act ? 1.0 / sqrt(limit_scaling(E[2] * r2)) : 0.0;
-    // apply: P <- dl P dl (column `lane`, the row factors read back from LDS), q <- dl q
+    const double el0 = even ? rsqrt(limit_scaling(E[0] * D)) : 0.0;
+    const double el1 = act ? rsqrt(limit_scaling(E[1] * r1)) : 0.0;
+    const double el2 = act ? rsqrt(limit_scaling(E[2] * r2)) : 0.0;
+    // apply: P <- ct_prev dl P dl (column `lane`, the row factors read back from LDS), q <- dl q
     lds_sync();
     sm.buf[lane] = dl;
     lds_sync();
+    const double dlc = dl * cpend;
     double cm2 = 0.0;
 #pragma unroll
     for (int i = 0; i < n; ++i) {
-      const double t = Pc[i] * (sm.buf[i] * dl);
+      const double t = Pc[i] * (sm.buf[i] * dlc);
       Pc[i] = t;
       cm2 = fmax(cm2, fabs(t));
     }
@@ -470,12 +479,13 @@ __device__ __forceinline__ bool setup_qp(const mpcqp_params& p, int b, const dou
     const double cn = wave_sum(act ? cm2 : 0.0) / n;
     const double qn = limit_scaling(wave_max(fabs(qv)));
     const double ct = 1.0 / limit_scaling(fmax(cn, qn));
-#pragma unroll
-    for (int i = 0; i < n; ++i) Pc[i] *= ct;
+    cpend = ct;
     qv *= ct;
     cmax = cm2 * ct;
     cscale *= ct;
   }
+#pragma unroll
+  for (int i = 0; i < n; ++i) Pc[i] *= cpend;
   __syncthreads();
   T.end(3);
   T.begin();
