@@ -207,15 +207,18 @@ struct Ctx {
     }
   }
   // (A^{-1} v)_lane
+  // No lane masks: the products read lanes 0..n-1 only, and the rows of lanes >= n are exactly
+  // zero (form() writes zeros there and every update of them multiplies by a zero), so those
+  // lanes return zero by themselves.
   __device__ __forceinline__ double inv_mul(double v) const {
     double w[4];
-    bcast<kNW>(act ? v : 0.0, w);
+    bcast<kNW>(v, w);
     double a[4] = {0.0, 0.0, 0.0, 0.0};
     Unroll<0, n>::run([&](auto jc) {
       constexpr int j = decltype(jc)::value;
       fmac_bc<j % 16>(a[j % 4], w[j / 16], r[j]);
     });
-    return act ? -((a[0] + a[1]) + (a[2] + a[3])) : 0.0;
+    return -((a[0] + a[1]) + (a[2] + a[3]));
   }
 };
 
