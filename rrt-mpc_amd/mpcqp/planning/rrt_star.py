@@ -118,12 +118,10 @@ def segment_is_free(occupancy: np.ndarray, start, end, collision_step: float) ->
     xs = np.linspace(start[0], end[0], samples + 1)
     ys = np.linspace(start[1], end[1], samples + 1)
     h, w = occupancy.shape
-    for x, y in zip(xs, ys):
-        xi = int(np.clip(round(x), 0, w - 1))
-        yi = int(np.clip(round(y), 0, h - 1))
-        if occupancy[yi, xi] == 0:
-            return False
-    return True
+    # vectorised: np.rint rounds half to even like Python's round(); same clip, same lookups
+    xi = np.clip(np.rint(xs), 0, w - 1).astype(np.intp)
+    yi = np.clip(np.rint(ys), 0, h - 1).astype(np.intp)
+    return not bool((occupancy[yi, xi] == 0).any())
 
 
 def _finish(occupancy, params: PlannerParameters, nodes: List[RRTStarNode], iterations: int,
