@@ -249,6 +249,21 @@ int mpcqp_rrt_plan(const mpcqp_rrt_params* p, int V, const uint8_t* occupancy, c
                    void* stream);
 
 /*
+ * Path extraction + shortcut pruning for the trees mpcqp_rrt_plan grew (replaces the host
+ * post-processing of src/planning/rrt_star.py:245-262 and _shortcut_prune :376-389; the
+ * Catmull-Rom smoothing :264-283 stays with the caller).  Same params, occupancy and
+ * nodes/count/meta as mpcqp_rrt_plan; prune = params.prune_path.
+ * Outputs (device), M = max_iterations + 2:
+ *   raw        V x M x 2   root -> goal node coordinates (raw_path)
+ *   raw_len    V           0 when the tree has no goal node
+ *   pruned     V x M x 2   the shortcut-pruned path (= raw when prune == 0 or raw_len <= 2)
+ *   pruned_len V
+ */
+int mpcqp_rrt_paths(const mpcqp_rrt_params* p, int V, int prune, const uint8_t* occupancy, const double* nodes,
+                    const int32_t* count, const int32_t* meta, double* raw, int32_t* raw_len, double* pruned,
+                    int32_t* pruned_len, void* stream);
+
+/*
  * Occupancy inflation: src/maps/inflate.py:18-51 (the fallback
  * dilation the reference uses without OpenCV) for B grids of height x width uint8
  * (1 = free, 0 = obstacle): out = 0 within the disk dx^2 + dy^2 <= r^2 of an obstacle.

@@ -279,9 +279,121 @@ __global__ __launch_bounds__(kPlanThreads) void k_rrt_plan(mpcqp_rrt_params p, i
   }
 }
 
+// Path extraction + shortcut pruning (rrt_star.py:245-262, _shortcut_prune :376-389) for the
+// trees k_rrt_plan grew, one workgroup per problem.  Thread 0 walks the parent chain from the
+// goal node into LDS; each pruning step i -> j takes the farthest j (> i + 1) whose segment is
+// free, else i + 1 -- the reference's "j from the end down to the first free segment" loop.
+// The candidates j are spread over the threads (each thread scans its own j's from the far
+// end, so its first free one is its largest) and a block max picks j.  Coordinates are copied,
+// never recomputed: raw and pruned paths are the host restatement's values bit for bit.
+__global__ __launch_bounds__(kPlanThreads) void k_rrt_paths(mpcqp_rrt_params p, int V, int prune,
+                                                             const uint8_t* __restrict__ occ,
+                                                             const double* __restrict__ nodes,
+                                                             const int32_t* __restrict__ count,
+                                                             const int32_t* __restrict__ meta,
+                                                             double* __restrict__ raw, int32_t* __restrict__ raw_len,
+                                                             double* __restrict__ pruned,
+                                                             int32_t* __restrict__ pruned_len) {
+  extern __shared__ double lds[];
+  __shared__ PlanSmem sm;
+  __shared__ int n_sh;
+  const int v = blockIdx.x;
+  if (v >= V) return;
+  const int tid = threadIdx.x;
+  const int M = p.max_iterations + 2;
+  double* X = lds;
+  double* Y = lds + M;
+  const double* tree = nodes + (size_t)v * M * 4;
+  const int goal = meta[2 * v + 1];
+  const int cnt = min(count[v], M);
+  if (tid == 0) {
+    int n = 0;
+    if (goal >= 0 && goal < cnt) {
+      // depth first (bounded by the node count: a parent chain never revisits a node)
+      for (int idx = goal; idx >= 0 && n < cnt; idx = (int)tree[4 * idx + 3]) ++n;
+      int idx = goal;
+      for (int k = n - 1; k >= 0; --k) {
+        X[k] = tree[4 * idx];
+        Y[k] = tree[4 * idx + 1];
+        idx = (int)tree[4 * idx + 3];
+      }
+    }
+    n_sh = n;
+  }
+  __syncthreads();
+  const int n = n_sh;
+  double* r = raw + (size_t)v * M * 2;
+  for (int k = tid; k < n; k += kPlanThreads) {
+    r[2 * k] = X[k];
+    r[2 * k + 1] = Y[k];
+  }
+  double* q = pruned + (size_t)v * M * 2;
+  if (!prune || n <= 2) {
+    for (int k = tid; k < n; k += kPlanThreads) {
+      q[2 * k] = X[k];
+      q[2 * k + 1] = Y[k];
+    }
+    if (tid == 0) {
+      raw_len[v] = n;
+      pruned_len[v] = n;
+    }
+    return;
+  }
+  const Grid g{occ, p.width, p.height, p.collision_step};
+  if (tid == 0) {
+    q[0] = X[0];
+    q[1] = Y[0];
+  }
+  int k = 1;
+  for (int i = 0; i < n - 1;) {  // every thread runs the same i sequence (block-uniform)
+    int best = i + 1;
+    for (int j = n - 1 - tid; j > i + 1; j -= kPlanThreads)
+      if (segment_free(g, X[i], Y[i], X[j], Y[j], 0, 1)) {
+        best = j;
+        break;
+      }
+    double key = -(double)best;
+    block_argmin(key, best, sm);
+    if (tid == 0) {
+      q[2 * k] = X[best];
+      q[2 * k + 1] = Y[best];
+    }
+    ++k;
+    i = best;
+  }
+  if (tid == 0) {
+    raw_len[v] = n;
+    pruned_len[v] = k;
+  }
+}
+
 }  // namespace
 
 extern "C" {
+
+int mpcqp_rrt_paths(const mpcqp_rrt_params* p, int V, int prune, const uint8_t* occupancy, const double* nodes,
+                    const int32_t* count, const int32_t* meta, double* raw, int32_t* raw_len, double* pruned,
+                    int32_t* pruned_len, void* stream) {
+  if (!p) return fail(MPCQP_E_ARG, "null params");
+  if (V < 0) return fail(MPCQP_E_ARG, "V must be >= 0");
+  if (V == 0) return MPCQP_OK;
+  if (!occupancy || !nodes || !count || !meta || !raw || !raw_len || !pruned || !pruned_len)
+    return fail(MPCQP_E_ARG, "null argument");
+  if (p->max_iterations < 1 || p->max_iterations > kMaxPlanIterations)
+    return fail(MPCQP_E_ARG, "max_iterations outside [1, " + std::to_string(kMaxPlanIterations) + "]");
+  if (p->width < 2 || p->height < 2) return fail(MPCQP_E_ARG, "grid must be at least 2 x 2");
+  const size_t lds = (size_t)(p->max_iterations + 2) * 2 * sizeof(double);
+  if (lds > 65536) {
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_rrt_paths),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return fail(MPCQP_E_HIP, std::string("hipFuncSetAttribute: ") + hipGetErrorString(e));
+  }
+  hipLaunchKernelGGL(k_rrt_paths, dim3(V), dim3(kPlanThreads), lds, static_cast<hipStream_t>(stream), *p, V,
+                     prune, occupancy, nodes, count, meta, raw, raw_len, pruned, pruned_len);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return fail(MPCQP_E_HIP, std::string("k_rrt_paths launch: ") + hipGetErrorString(e));
+  return MPCQP_OK;
+}
 
 int mpcqp_rrt_plan(const mpcqp_rrt_params* p, int V, const uint8_t* occupancy, const double* start_goal,
                    const double* samples, const uint64_t* rng_state, double* nodes, int32_t* count, int32_t* meta,

@@ -193,6 +193,8 @@ _SYMBOLS = {
                                ctypes.c_int, ctypes.c_double, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
                                ctypes.c_void_p], ctypes.c_int),
     "mpcqp_rrt_plan": ([ctypes.POINTER(MpcqpRrtParams), ctypes.c_int] + [ctypes.c_void_p] * 8, ctypes.c_int),
+    "mpcqp_rrt_paths": ([ctypes.POINTER(MpcqpRrtParams), ctypes.c_int, ctypes.c_int] + [ctypes.c_void_p] * 9,
+                        ctypes.c_int),
     "mpcqp_inflate": ([ctypes.c_int] * 4 + [ctypes.c_void_p] * 3, ctypes.c_int),
     "mpcqp_model_buffer": ([ctypes.c_void_p], ctypes.c_void_p),
     "mpcqp_model_stride": ([ctypes.c_int], ctypes.c_int),

@@ -50,9 +50,12 @@ class Swarm:
         self.max_replans = int(max_replans)
 
     def _plan(self, starts, goals, seeds):
-        res = self.planner.plan_batch(starts, goals, seeds)
-        paths = [r.path if r.success else [tuple(s)] for r, s in zip(res, starts)]
-        return res, paths
+        """Final paths of every problem (growth, extraction and pruning on the device);
+        returns (success mask, paths with the start alone where no plan was found)."""
+        found = self.planner.paths_batch(starts, goals, seeds)
+        ok = np.array([p is not None for p in found], dtype=bool)
+        paths = [p if p is not None else [tuple(s)] for p, s in zip(found, starts)]
+        return ok, paths
 
     def run(self, starts: np.ndarray, goals: np.ndarray, seeds=None, *, sim_steps: Optional[int] = None,
             check_every: int = 10) -> SwarmResult:
@@ -64,8 +67,7 @@ class Swarm:
         total = int(self.mpc.sim_steps if sim_steps is None else sim_steps)
         t = {}
         t0 = time.perf_counter()
-        res, paths = self._plan(starts, goals, seeds)
-        planned = np.array([r.success for r in res])
+        planned, paths = self._plan(starts, goals, seeds)
         t["plan_s"] = time.perf_counter() - t0
         t0 = time.perf_counter()
         self.fleet.reset_from_plans(paths, starts, goals, max_steps=total, device_reference=True)
@@ -114,8 +116,7 @@ class Swarm:
         b = self.fleet.buffers()
         state = b["state"][:len(replans)].cpu().numpy()
         starts = state[idx, :2]
-        res, paths = self._plan(starts, goals[idx], seeds[idx] + 7919 * (replans[idx] + 1))
-        ok = np.array([r.success for r in res])
+        ok, paths = self._plan(starts, goals[idx], seeds[idx] + 7919 * (replans[idx] + 1))
         replans[idx] += 1
         if not ok.any():
             return

@@ -238,6 +238,57 @@ class BatchedRRTStarPlanner:
                                         meta.data_ptr(), ctypes.c_void_p(stream.cuda_stream)), "mpcqp_rrt_plan")
         return nodes[:V], count[:V], meta[:V]
 
+    def extract(self, nodes, count, meta, stream=None):
+        """Raw and shortcut-pruned paths of grown trees on the device (``mpcqp_rrt_paths``,
+        ``rrt_star.py:245-262,376-389``): device tensors raw (V, M, 2), raw_len (V,),
+        pruned (V, M, 2), pruned_len (V,)."""
+        torch = self._torch
+        V = int(nodes.shape[0])
+        M = int(self.params.max_iterations) + 2
+        dev = self.device
+        raw = torch.empty((max(V, 1), M, 2), dtype=torch.float64, device=dev)
+        pruned = torch.empty_like(raw)
+        raw_len = torch.empty((max(V, 1),), dtype=torch.int32, device=dev)
+        pruned_len = torch.empty_like(raw_len)
+        if stream is None:
+            stream = torch.cuda.current_stream(dev)
+        with torch.cuda.device(dev):
+            _lib.check(_lib.lib().mpcqp_rrt_paths(ctypes.byref(self._c), V, int(bool(self.params.prune_path)),
+                                                  self._occ.data_ptr(), nodes.data_ptr(), count.data_ptr(),
+                                                  meta.data_ptr(), raw.data_ptr(), raw_len.data_ptr(),
+                                                  pruned.data_ptr(), pruned_len.data_ptr(),
+                                                  ctypes.c_void_p(stream.cuda_stream)), "mpcqp_rrt_paths")
+        return raw[:V], raw_len[:V], pruned[:V], pruned_len[:V]
+
+    def paths_batch(self, starts, goals, seeds=None) -> List[Optional[List[Tuple[float, float]]]]:
+        """The final path of ``plan(start, goal)`` for every problem (None where no goal was
+        reached), without building the tree on the host: growth, extraction and pruning run on
+        the device; only the pruned paths come back for the Catmull-Rom smoothing
+        (``rrt_star.py:264-283``).  Equal to ``plan_batch(...)[v].path``."""
+        starts = np.asarray(starts, dtype=float).reshape(-1, 2)
+        V = len(starts)
+        if seeds is None:
+            seeds = [self.params.random_seed] * V
+        nodes, count, meta = self.grow(starts, goals, seeds)
+        _, _, pruned, plen = self.extract(nodes, count, meta)
+        plen = plen.cpu().numpy()
+        L = int(plen.max()) if V else 0
+        pts = pruned[:, :L].cpu().numpy()
+        out: List[Optional[List[Tuple[float, float]]]] = []
+        for v in range(V):
+            n = int(plen[v])
+            if n == 0:
+                out.append(None)
+                continue
+            working = [tuple(map(float, pt)) for pt in pts[v, :n]]
+            if n >= 2 and self.params.spline_samples > 1:
+                spline = catmull_rom_spline(working, samples_per_segment=self.params.spline_samples,
+                                            alpha=self.params.spline_alpha, dedupe_tol=self.params.dedupe_tolerance)
+                if len(spline) >= 2:
+                    working = [tuple(map(float, pt)) for pt in spline]
+            out.append(working)
+        return out
+
     def plan_batch(self, starts, goals, seeds=None) -> List[PlanResult]:
         """``plan(start, goal)`` for every problem (seed defaults to ``params.random_seed``)."""
         starts = np.asarray(starts, dtype=float).reshape(-1, 2)

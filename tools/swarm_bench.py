@@ -78,6 +78,13 @@ def main() -> None:
         out.setdefault("planner", []).append({"trees": V, "seconds": dt, "trees_per_s": V / dt,
                                               "note": "device-side sampling from each seed's numpy PCG64 state; host post-processing excluded"})
         print(json.dumps(out["planner"][-1]), flush=True)
+        # whole plans: device extraction + pruning (paths_batch) vs host post-processing (plan_batch)
+        for name, fn in (("paths_batch", pl.paths_batch), ("plan_batch", pl.plan_batch)):
+            t0 = time.perf_counter()
+            fn(starts, goals, np.arange(V))
+            dt = time.perf_counter() - t0
+            out.setdefault("plans", []).append({"api": name, "trees": V, "seconds": dt, "plans_per_s": V / dt})
+            print(json.dumps(out["plans"][-1]), flush=True)
     starts, goals = pairs(occ, 8, 9)
     t0 = time.perf_counter()
     for v in range(8):
