@@ -75,15 +75,17 @@ def catmull_rom_spline(points, *, samples_per_segment: int = 20, alpha: float = 
         t3 = knot(t2, p2, p3)
         d01, d12, d23 = max(t1 - t0, eps), max(t2 - t1, eps), max(t3 - t2, eps)
         d02, d13 = max(t2 - t0, eps), max(t3 - t1, eps)
-        for t in np.linspace(t1, t2, max(2, samples_per_segment + 1), endpoint=False):
-            a1 = (t1 - t) / d01 * p0 + (t - t0) / d01 * p1
-            a2 = (t2 - t) / d12 * p1 + (t - t1) / d12 * p2
-            a3 = (t3 - t) / d23 * p2 + (t - t2) / d23 * p3
-            b1 = (t2 - t) / d02 * a1 + (t - t0) / d02 * a2
-            b2 = (t3 - t) / d13 * a2 + (t - t1) / d13 * a3
-            out.append((t2 - t) / d12 * b1 + (t - t1) / d12 * b2)
-    out.append(pts[-1])
-    return np.asarray(out)
+        # all samples of the segment at once: the same IEEE operations in the same order per
+        # sample as the reference's scalar loop (numpy does not contract), so bit-identical
+        t = np.linspace(t1, t2, max(2, samples_per_segment + 1), endpoint=False)[:, None]
+        a1 = (t1 - t) / d01 * p0 + (t - t0) / d01 * p1
+        a2 = (t2 - t) / d12 * p1 + (t - t1) / d12 * p2
+        a3 = (t3 - t) / d23 * p2 + (t - t2) / d23 * p3
+        b1 = (t2 - t) / d02 * a1 + (t - t0) / d02 * a2
+        b2 = (t3 - t) / d13 * a2 + (t - t1) / d13 * a3
+        out.append((t2 - t) / d12 * b1 + (t - t1) / d12 * b2)
+    out.append(pts[-1][None, :])
+    return np.concatenate(out)
 
 
 __all__ = ["resample_polyline", "heading_from_path", "curvature_slowdown", "catmull_rom_spline"]
