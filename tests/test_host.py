@@ -138,6 +138,59 @@ def test_scenario_branches_match_reference_golden(golden):
         np.testing.assert_array_equal(build_reference(sp, 15.0, 20, 0.1), g["ref"][g["ref_off"][i]: g["ref_off"][i + 1]])
 
 
+def test_catmull_rom_vectorised_equals_per_sample_loop():
+    """The per-segment vectorised smoothing == the reference's per-sample loop
+    (rrt_star.py:93-159, restated scalar here), bit for bit, on duplicates, collinear and
+    integer points and alpha in {0, 0.5, 1}."""
+    from mpcqp.common.geometry import catmull_rom_spline
+
+    def scalar(points, S, alpha, eps=1e-9, tol=1e-9):
+        keep = [np.asarray(points[0], float)]
+        for p in np.asarray(points, float)[1:]:
+            if np.linalg.norm(p - keep[-1]) > tol:
+                keep.append(p)
+        pts = np.asarray(keep)
+        if len(pts) <= 2:  # straight-line branches, not the loop under test
+            return None
+        ext = np.vstack([pts[0], pts, pts[-1]])
+        out = []
+        for i in range(len(pts) - 1):
+            p0, p1, p2, p3 = ext[i:i + 4]
+            ts = [0.0]
+            for a, b in ((p0, p1), (p1, p2), (p2, p3)):
+                d = np.linalg.norm(b - a)
+                ts.append(ts[-1] + ((d ** alpha) if d > eps else eps))
+            t0, t1, t2, t3 = ts
+            d01, d12, d23 = max(t1 - t0, eps), max(t2 - t1, eps), max(t3 - t2, eps)
+            d02, d13 = max(t2 - t0, eps), max(t3 - t1, eps)
+            for t in np.linspace(t1, t2, max(2, S + 1), endpoint=False):
+                a1 = (t1 - t) / d01 * p0 + (t - t0) / d01 * p1
+                a2 = (t2 - t) / d12 * p1 + (t - t1) / d12 * p2
+                a3 = (t3 - t) / d23 * p2 + (t - t2) / d23 * p3
+                b1 = (t2 - t) / d02 * a1 + (t - t0) / d02 * a2
+                b2 = (t3 - t) / d13 * a2 + (t - t1) / d13 * a3
+                out.append((t2 - t) / d12 * b1 + (t - t1) / d12 * b2)
+        out.append(pts[-1])
+        return np.asarray(out)
+
+    rng = np.random.default_rng(5)
+    for k in range(60):
+        pts = rng.uniform(0, 80, (int(rng.integers(3, 25)), 2))
+        if k % 3 == 0:
+            pts[1] = pts[0]
+            pts[-1] = pts[-2] + 1e-12
+        if k % 4 == 0:
+            pts = np.round(pts)
+        if k % 5 == 0:
+            pts[:, 1] = 7.0
+        for alpha in (0.0, 0.5, 1.0):
+            S = int(rng.integers(1, 25))
+            want = scalar(pts, S, alpha)
+            got = catmull_rom_spline(pts, samples_per_segment=S, alpha=alpha)
+            if want is not None:
+                np.testing.assert_array_equal(got, want)
+
+
 def test_scenarios_shapes_and_determinism():
     from mpcqp import scenarios
 
