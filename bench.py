@@ -1,16 +1,29 @@
 #!/usr/bin/env python3
 """Benchmark: batched bicycle-MPC QP solves/s on MI355X (BASELINE.json metric).
 
-One "step" = one pass of the hot path over one batch resident in HBM:
-K1 ``k_build`` (unwrap + linearize) + K2 ``k_solve`` (condense + ADMM/OSQP + polish)
-for every QP of the batch.  Default workload = BASELINE config 3 (B=4096 randomised
-RRT*-branch references, horizon 20) per GPU; with N GPUs each rank solves its own
-contiguous shard of a 4096*N batch (weak scaling, no data-path collective).
+One "step" = one pass of the hot path over one batch resident in HBM: ``mpcqp_build`` +
+``mpcqp_solve`` (window -> LTV model -> condense -> ADMM/OSQP -> polish) for every QP of the
+shard.  Default workload = BASELINE config 3 (B=4096 randomised RRT*-branch references,
+horizon 20) per GPU.
+
+Multi-GPU (one process per GPU, ``torch.distributed``; backend ``nccl`` = RCCL):
+  * weak scaling (default): every rank solves its own contiguous shard of a ``batch x world``
+    global batch;
+  * strong scaling (``--global-batch G``, e.g. config 4: 16384 over 2/4/8 GPUs): the ranks
+    split a fixed global batch contiguously.
+There is no data-path collective (the QPs are independent).  Around the timed region: a barrier
+on both sides, a MAX of the elapsed time and a SUM of the counters; after it one ``all_gather``
+of u0/status whose global result rank 0 spot-checks against the C restatement.
 
     python bench.py --gpus 1 --steps 20 --warmup 3
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+    python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N --config config4 --global-batch 16384
 
 Prints ONE JSON line on rank 0 (driver contract; roofline + cpu_baseline objects).
+
+The distributed helpers (``shard_bounds``, ``DistContext``, ``timed_steps``, ``reduce_stats``,
+``gather_rows``, ``spot_check``) are plain functions: tests/test_distributed.py drives the same
+ones with the gloo backend on CPU.
 """
 from __future__ import annotations
 
@@ -22,6 +35,7 @@ import platform
 import sys
 import time
 from pathlib import Path
+from typing import Callable, Dict, List, Optional, Tuple
 
 import numpy as np
 
@@ -31,6 +45,8 @@ sys.path.insert(0, str(ROOT))
 
 FP64_PEAK_TFLOPS = 78.6  # MI355X FP64 dense (vector == matrix), AMD spec
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E, MI355X_MICROARCH.md
+BASELINE_METRIC = "MPC QP solves/s (horizon=20, batch=4096) @1/2/4/8 GPU; rel-err vs OSQP"
+DEFAULT_BATCH = {"config2": 1024, "config3": 4096, "config4": 16384}
 
 
 def qp_bytes(N: int) -> int:
@@ -39,7 +55,7 @@ def qp_bytes(N: int) -> int:
 
 
 def qp_flops(N: int, iters: np.ndarray, scaling: int = 10, check: int = 25) -> np.ndarray:
-    """Algorithmic FP64 flops per QP as implemented (DESIGN.md §5), from the kernel's counters
+    """Algorithmic FP64 flops per QP as implemented (DESIGN.md §3), from the kernel's counters
     (ADMM iterations, polish passes, factorizations + passes, line-search trials):
       setup      condensing 50 N (n+1) + Ruiz `scaling` x 3 n^2
       ADMM       (factorizations - passes) x (n^3 + 4 n^2): explicit SPD inverse by the sweep;
@@ -58,25 +74,141 @@ def qp_flops(N: int, iters: np.ndarray, scaling: int = 10, check: int = 25) -> n
     return f
 
 
-def make_batch(config: str, batch_per_gpu: int, world: int, rank: int):
+# ------------------------------------------------------------------ workload + sharding
+def make_global_batch(config: str, total: int):
     from mpcqp import scenarios
 
-    total = batch_per_gpu * world
-    if config == "config2":
-        b = scenarios.config2(total)
-    elif config == "config3":
-        b = scenarios.config3(total)
-    elif config == "config4":
-        b = scenarios.config4(total)
-    else:
+    if config not in scenarios.CONFIGS:
         raise SystemExit(f"unknown config {config}")
-    sl = slice(rank * batch_per_gpu, (rank + 1) * batch_per_gpu)
-    return b.x0[sl], b.ref[sl], b.u_prev[sl], b.horizon, b.name
+    return scenarios.CONFIGS[config](total)
 
 
-BASELINE_METRIC = "MPC QP solves/s (horizon=20, batch=4096) @1/2/4/8 GPU; rel-err vs OSQP"
+def shard_bounds(total: int, world: int, rank: int) -> Tuple[int, int]:
+    """Contiguous shard [lo, hi) of rank `rank`; the first total % world ranks
+    take one QP more, so any total splits."""
+    base, extra = divmod(int(total), int(world))
+    lo = rank * base + min(rank, extra)
+    return lo, lo + base + (1 if rank < extra else 0)
 
 
+def shard_counts(total: int, world: int) -> List[int]:
+    return [b - a for a, b in (shard_bounds(total, world, r) for r in range(world))]
+
+
+def make_batch(config: str, batch_per_gpu: int, world: int, rank: int):
+    """Weak-scaling shard: rank `rank`'s contiguous part of a batch_per_gpu x world global batch."""
+    b = make_global_batch(config, batch_per_gpu * world)
+    lo, hi = shard_bounds(batch_per_gpu * world, world, rank)
+    return b.x0[lo:hi], b.ref[lo:hi], b.u_prev[lo:hi], b.horizon, b.name
+
+
+class DistContext:
+    """Rank / world of this process and the collectives the bench uses (no-ops at world 1).
+    Tensors live on `device` (CUDA for nccl, CPU for gloo)."""
+
+    def __init__(self, world: int = 1, rank: int = 0, local_rank: int = 0, backend: Optional[str] = None,
+                 device=None) -> None:
+        self.world, self.rank, self.local_rank, self.backend, self.device = world, rank, local_rank, backend, device
+        self._dist = None
+        if world > 1:
+            import torch.distributed as dist
+
+            self._dist = dist
+
+    @classmethod
+    def from_env(cls, backend: str = "nccl") -> "DistContext":
+        """One process per GPU as torch.distributed.run starts it (RANK / LOCAL_RANK / WORLD_SIZE)."""
+        import torch
+        import torch.distributed as dist
+
+        world = int(os.environ.get("WORLD_SIZE", "1"))
+        rank = int(os.environ.get("RANK", "0"))
+        local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+        # one process per GPU; ranks beyond the visible devices wrap (rehearsal on one GPU)
+        dev_index = local_rank % max(1, torch.cuda.device_count())
+        device = torch.device("cuda", dev_index)
+        if world > 1:
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            torch.cuda.set_device(dev_index)
+            if backend == "nccl":
+                dist.init_process_group("nccl", device_id=device)
+            else:
+                dist.init_process_group("gloo")
+        torch.cuda.set_device(device)
+        ctx = cls(world, rank, local_rank, backend if world > 1 else None, device)
+        # gloo collectives take host tensors
+        ctx.coll_device = device if backend == "nccl" else torch.device("cpu")
+        return ctx
+
+    coll_device = None
+
+    def _cdev(self):
+        return self.coll_device if self.coll_device is not None else self.device
+
+    def barrier(self) -> None:
+        if self._dist is not None:
+            self._dist.barrier()
+
+    def all_reduce(self, t, op: str):
+        if self._dist is not None:
+            self._dist.all_reduce(t, op=self._dist.ReduceOp.MAX if op == "max" else self._dist.ReduceOp.SUM)
+        return t
+
+    def all_gather(self, t) -> list:
+        if self._dist is None:
+            return [t]
+        parts = [t.new_empty(t.shape) for _ in range(self.world)]
+        self._dist.all_gather(parts, t)
+        return parts
+
+    def close(self) -> None:
+        if self._dist is not None:
+            self._dist.destroy_process_group()
+
+
+def timed_steps(step: Callable[[int], None], steps: int, warmup: int, ctx: DistContext,
+                sync: Callable[[], None] = lambda: None) -> float:
+    """W untimed warmup steps, then EXACTLY `steps` steps bracketed by a barrier + device sync on
+    both sides; returns this rank's elapsed seconds (bench.py contract)."""
+    for _ in range(warmup):
+        step(-1)
+    sync()
+    ctx.barrier()
+    sync()
+    t0 = time.perf_counter()
+    for k in range(steps):
+        step(k)
+    sync()
+    ctx.barrier()
+    return time.perf_counter() - t0
+
+
+def reduce_stats(ctx: DistContext, elapsed: float, sums: List[float]) -> Tuple[float, List[float]]:
+    """MAX over ranks of the elapsed time, SUM of the counters."""
+    import torch
+
+    t = torch.tensor([elapsed], dtype=torch.float64, device=ctx._cdev())
+    s = torch.tensor([float(v) for v in sums], dtype=torch.float64, device=ctx._cdev())
+    ctx.all_reduce(t, "max")
+    ctx.all_reduce(s, "sum")
+    return float(t.item()), [float(v) for v in s.cpu().tolist()]
+
+
+def gather_rows(ctx: DistContext, t, counts: List[int]):
+    """All ranks' shards of a row-distributed tensor, concatenated in rank order (shards of
+    unequal length are padded to the largest for the collective)."""
+    import torch
+
+    if ctx.world == 1:
+        return t
+    m = max(counts)
+    pad = t.new_zeros((m,) + tuple(t.shape[1:]))
+    pad[: t.shape[0]] = t
+    parts = ctx.all_gather(pad.to(ctx._cdev()))
+    return torch.cat([p[:c] for p, c in zip(parts, counts)])
+
+
+# ------------------------------------------------------------------ checker / CPU baseline leg
 def _cpu_model() -> str:
     try:
         for line in open("/proc/cpuinfo"):
@@ -87,22 +219,49 @@ def _cpu_model() -> str:
     return platform.processor() or platform.machine()
 
 
-def cpu_baseline(params, x0, ref, u_prev, seconds: float, gpu_U=None, gpu_active=None):
-    """The C restatement (oracle/, kind "port") on the host cores, bounded sample.
+def host_threads() -> Tuple[int, int]:
+    """(threads to use, cores visible to this process).  All visible cores, unless the host
+    assigns this job a share through OMP_NUM_THREADS (the GPU box sets 16 per GPU)."""
+    try:
+        visible = len(os.sched_getaffinity(0))
+    except AttributeError:  # pragma: no cover
+        visible = os.cpu_count() or 1
+    env = os.environ.get("OMP_NUM_THREADS")
+    threads = min(visible, int(env)) if env and env.isdigit() and int(env) > 0 else visible
+    return threads, visible
 
-    As the checker, it also gives the GPU batch's rel-err: the C restatement's polish ends at
-    the exact optimum, which is the OSQP+polish optimum of the reference (a strictly convex QP)."""
+
+def spot_check(params, x0, ref, u_prev, U, active, status, idx) -> dict:
+    """Checker: the GPU solutions of QPs `idx` against the C restatement, whose polish ends at the
+    exact optimum of the QP (strictly convex: the same optimum OSQP+polish returns in the
+    reference).  Parity against OSQP itself is unpinned here (OSQP is not installed)."""
     sys.path.insert(0, str(ROOT / "oracle"))
     import cpu_solver
 
-    try:
-        cores = len(os.sched_getaffinity(0))
-    except AttributeError:  # pragma: no cover
-        cores = os.cpu_count() or 1
-    threads = max(1, min(cores, int(os.environ.get("OMP_NUM_THREADS", cores)), 16))
+    idx = np.asarray(idx)
+    threads, _ = host_threads()
+    out = cpu_solver.cpu_solve(params, x0[idx], ref[idx], u_prev[idx], nthreads=threads)
+    Uc = out["U"].reshape(len(idx), -1)
+    Ug = np.asarray(U)[idx].reshape(len(idx), -1)
+    err = np.abs(Ug - Uc).max(axis=1) / np.maximum(1.0, np.abs(Uc).max(axis=1))
+    return {
+        "vs": "exact optimum (C restatement's polish, oracle/mpcqp_cpu.c); OSQP itself is absent, "
+              "so parity with OSQP's own iterates is unpinned",
+        "qps": int(len(idx)),
+        "max_rel_err_U": float(err.max()) if len(idx) else 0.0,
+        "active_set_mismatches": int((np.asarray(active)[idx] != out["active"]).any(axis=1).sum()),
+        "status_mismatches": int((np.asarray(status)[idx] != out["status"]).sum()),
+    }
+
+
+def cpu_baseline(params, x0, ref, u_prev, seconds: float) -> dict:
+    """The C restatement (oracle/, kind "port") on the host cores, bounded sample."""
+    sys.path.insert(0, str(ROOT / "oracle"))
+    import cpu_solver
+
+    threads, visible = host_threads()
     cpu_solver.cpu_solve(params, x0[:64], ref[:64], u_prev[:64], nthreads=threads)  # warm (build + page-in)
-    done, t0 = 0, time.perf_counter()
-    solved = 0
+    done, solved, t0 = 0, 0, time.perf_counter()
     while True:
         out = cpu_solver.cpu_solve(params, x0, ref, u_prev, nthreads=threads)
         done += len(x0)
@@ -116,26 +275,74 @@ def cpu_baseline(params, x0, ref, u_prev, seconds: float, gpu_U=None, gpu_active
         out1 = cpu_solver.cpu_solve(params, x0[:256], ref[:256], u_prev[:256], nthreads=1)
         n1 += int((out1["status"] == 1).sum())
     dt1 = time.perf_counter() - t1
-    parity = None
-    if gpu_U is not None:
-        Uc = out["U"]
-        parity = {
-            "vs": "exact optimum (C restatement's polish; = the reference's OSQP+polish optimum)",
-            "qps": int(len(Uc)),
-            "max_rel_err_U": float(np.max(np.abs(gpu_U - Uc).reshape(len(Uc), -1).max(axis=1)
-                                          / np.maximum(1.0, np.abs(Uc).reshape(len(Uc), -1).max(axis=1)))),
-            "active_set_mismatches": int((gpu_active != out["active"]).any(axis=1).sum()),
-        }
-    return parity, {
+    return {
         "value": solved / dt,
         "unit": "QP/s",
         "cores": threads,
         "kind": "port",
+        "threads": threads,
+        "host_cores_visible": visible,
         "value_1core": n1 / dt1,
+        "value_all_visible_cores_linear": n1 / dt1 * visible,
         "cpu_model": _cpu_model(),
-        "sample": f"{done} QPs ({done // len(x0)} passes over this rank's batch) in {dt:.1f} s, "
-                  f"C restatement of the same ADMM+polish algorithm (oracle/mpcqp_cpu.c, OpenMP), "
-                  f"host {platform.processor() or platform.machine()}",
+        "sample": f"{done} QPs ({done // len(x0)} passes over this rank's batch) in {dt:.1f} s on {threads} "
+                  f"OpenMP threads ({visible} cores visible; the GPU box assigns OMP_NUM_THREADS per GPU), "
+                  f"C restatement of the same ADMM+polish algorithm (oracle/mpcqp_cpu.c)",
+    }
+
+
+def config1_closed_loop() -> dict:
+    """BASELINE config 1: the default single-vehicle closed loop at horizon 10,
+    100 control steps (the loop stops at the goal after ~65 solves), through the drop-in
+    TrajectoryTracker.track (one B=1 GPU solve per step, the reference's call pattern,
+    control_stage.py:100-150) and through the C restatement's solve on one core (checker leg)."""
+    from types import SimpleNamespace
+
+    from mpcqp import scenarios
+    from mpcqp.config import MPCConfig, VizConfig
+    from mpcqp.pipeline.control_stage import TrajectoryTracker
+
+    sys.path.insert(0, str(ROOT / "oracle"))
+    import cpu_solver
+    import mpc_oracle as mo
+
+    plan = scenarios.load_default_plan()
+    path = [tuple(map(float, q)) for q in plan["path"]]
+    mpc = MPCConfig(horizon=10, sim_steps=100)
+    tracker = TrajectoryTracker(mpc, VizConfig())
+    planning = SimpleNamespace(plan=SimpleNamespace(success=True, path=path))
+    maps = SimpleNamespace(start=tuple(plan["start"]), goal=tuple(plan["goal"]))
+    tracker.track(planning, maps, map_resolution=0.8, visualize=False)  # warm (workspace, graph)
+    t0 = time.perf_counter()
+    states = tracker.track(planning, maps, map_resolution=0.8, visualize=False).states
+    gpu_s = time.perf_counter() - t0
+
+    params = mpc.to_parameters(0.8)
+    from mpcqp.control.ref_builder import build_reference
+
+    ref_g = build_reference(plan["path"], mpc.v_px_s, 10, mpc.dt)
+
+    def c_solve(p, state, window, u_prev):
+        o = cpu_solver.cpu_solve(p, state[None], window[None], u_prev[None], nthreads=1)
+        if int(o["status"][0]) not in (1, 2):
+            return None, None, None
+        return o["u0"][0], o["X"][0], o["U"][0]
+
+    t0 = time.perf_counter()
+    c_states = mo.track_loop(params, ref_g, plan["start"], float(plan["yaw0"]), plan["goal"], 100, c_solve)
+    cpu_s = time.perf_counter() - t0
+    dev = max(float(np.abs(np.asarray(states) - np.asarray(c_states)).max()), 0.0) \
+        if len(states) == len(c_states) else None
+    return {
+        "workload": "config1: default plan, horizon 10, sim_steps 100, one vehicle",
+        "solves": len(states),
+        "gpu_b1_shim_s": gpu_s,
+        "gpu_ms_per_step": 1e3 * gpu_s / max(1, len(states)),
+        "cpu_restatement_1core_s": cpu_s,
+        "cpu_ms_per_step": 1e3 * cpu_s / max(1, len(c_states)),
+        "max_state_diff_px": dev,
+        "note": "sequential loop: one QP per step, so a B=1 launch + host sync per step bounds the GPU "
+                "figure; the batched path is the fleet (DESIGN.md §7)",
     }
 
 
@@ -151,13 +358,16 @@ def load_pmc_traffic(N: int, batch: int):
         return None
 
 
+# ------------------------------------------------------------------ main
 def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--config", default="config3", choices=["config2", "config3", "config4"])
-    ap.add_argument("--batch", type=int, default=0, help="QPs per GPU (default: the config's)")
+    ap.add_argument("--config", default="config3", choices=sorted(DEFAULT_BATCH))
+    ap.add_argument("--batch", type=int, default=0, help="QPs per GPU, weak scaling (default: the config's)")
+    ap.add_argument("--global-batch", type=int, default=0,
+                    help="strong scaling: a fixed global batch split over the ranks (e.g. 16384 for config 4)")
     ap.add_argument("--method", default="admm", choices=["admm", "newton"])
     ap.add_argument("--polish-from", type=int, default=None,
                     help="ADMM iteration of the first early polish attempt (default: the library's; 0 = off)")
@@ -166,36 +376,31 @@ def main() -> int:
     ap.add_argument("--set", action="append", default=[], metavar="KEY=VALUE",
                     help="development: override a solver setting of mpcqp_params (repeatable)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline sample length (0 = skip)")
+    ap.add_argument("--check-sample", type=int, default=512, help="QPs of the gathered result rank 0 checks")
+    ap.add_argument("--no-config1", action="store_true", help="skip the config-1 closed-loop line")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="torch.distributed backend for N > 1 (nccl = RCCL; gloo only to rehearse "
                          "several ranks on one GPU)")
     args = ap.parse_args()
 
     import torch
-    import torch.distributed as dist
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    # one process per GPU; ranks beyond the visible devices wrap (rehearsal on one GPU)
-    dev_index = local_rank % max(1, torch.cuda.device_count())
-    if world > 1:
-        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        torch.cuda.set_device(dev_index)
-        if args.backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", dev_index))
-        else:
-            dist.init_process_group("gloo")
-    device = torch.device("cuda", dev_index)
-    torch.cuda.set_device(device)
+    ctx = DistContext.from_env(args.backend)
+    world, rank, device = ctx.world, ctx.rank, ctx.device
 
     from mpcqp import _lib
     from mpcqp.config import MPCConfig
     from mpcqp.control.mpc_controller import BatchedMPCController
 
-    default_batch = {"config2": 1024, "config3": 4096, "config4": 16384}[args.config]
-    B = args.batch or default_batch
-    x0, ref, u_prev, N, name = make_batch(args.config, B, world, rank)
+    strong = args.global_batch > 0
+    per_gpu = args.batch or DEFAULT_BATCH[args.config]
+    total = args.global_batch if strong else per_gpu * world
+    batch = make_global_batch(args.config, total)
+    N, name = batch.horizon, batch.name
+    lo, hi = shard_bounds(total, world, rank)
+    counts = shard_counts(total, world)
+    B = hi - lo
+    x0, ref, u_prev = batch.x0[lo:hi], batch.ref[lo:hi], batch.u_prev[lo:hi]
     params = MPCConfig(horizon=N).to_parameters(0.8)
     extra = {} if args.polish_from is None else {"polish_from": args.polish_from}
     if args.polish_near is not None:
@@ -203,15 +408,17 @@ def main() -> int:
     for kv in args.set:
         k, v = kv.split("=", 1)
         extra[k] = float(v) if "." in v or "e" in v else int(v)
-    ctrl = BatchedMPCController(params, B, device=device, method=args.method, **extra)
+    ctrl = BatchedMPCController(params, max(1, B), device=device, method=args.method, **extra)
     x0_t = torch.from_numpy(x0).to(device)
     ref_t = torch.from_numpy(ref).to(device)
     up_t = torch.from_numpy(u_prev).to(device)
     L = _lib.lib()
     stream = torch.cuda.current_stream(device)
     s = ctypes.c_void_p(stream.cuda_stream)
+    events = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
 
-    def step(ev=None):
+    def step(k: int) -> None:
+        ev = events[k] if k >= 0 else None
         if ev is not None:
             ev[0].record(stream)
         _lib.check(L.mpcqp_build(ctrl._ws, B, x0_t.data_ptr(), ref_t.data_ptr(), up_t.data_ptr(), s), "build")
@@ -223,47 +430,31 @@ def main() -> int:
         if ev is not None:
             ev[2].record(stream)
 
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize(device)
-    events = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize(device)
-    t0 = time.perf_counter()
-    for k in range(args.steps):
-        step(events[k])
-    torch.cuda.synchronize(device)
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
+    elapsed = timed_steps(step, args.steps, args.warmup, ctx, lambda: torch.cuda.synchronize(device))
     k1_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in events]))
     k2_ms = float(np.mean([e[1].elapsed_time(e[2]) for e in events]))
 
     status = ctrl._status[:B].cpu().numpy()
     iters = ctrl._iters[:B].cpu().numpy()
-    solved = int((status == 1).sum())
     flops = qp_flops(N, iters)
-    stats = torch.tensor([elapsed, float(solved), float(flops.sum()), float(iters[:, 0].sum()),
-                          float(iters[:, 1].sum())], dtype=torch.float64, device=device)
-    if world > 1:
-        tmax = stats[:1].clone()
-        dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
-        rest = stats[1:].clone()
-        dist.all_reduce(rest, op=dist.ReduceOp.SUM)
-        stats = torch.cat([tmax, rest])
-    T, solved_all, flops_all, admm_all, pol_all = (float(v) for v in stats.cpu().tolist())
+    T, (solved_all, flops_all, admm_all, pol_all) = reduce_stats(
+        ctx, elapsed, [float((status == 1).sum()), float(flops.sum()), float(iters[:, 0].sum()),
+                       float(iters[:, 1].sum())])
+    # end-of-run gather of the per-QP results (u0, status, U, active) to every rank
+    g = {k: gather_rows(ctx, t[:B], counts) for k, t in
+         (("u0", ctrl._u0), ("status", ctrl._status), ("U", ctrl._U), ("active", ctrl._active))}
+    g = {k: v.cpu().numpy() for k, v in g.items()}
 
     if rank == 0:
         value = solved_all * args.steps / T
         ms_per_step = 1000.0 * T / args.steps
         achieved_tf = float(flops.sum()) / (k2_ms * 1e-3) / 1e12  # rank-0 K2 launch, algorithmic flops
-        hbm_gbs = B * qp_bytes(N) / (ms_per_step * 1e-3) / 1e9
+        hbm_gbs = total * qp_bytes(N) / (ms_per_step * 1e-3) / 1e9
         pmc = load_pmc_traffic(N, B) or {}
         traffic = pmc.get("k_solve_hbm_bytes_per_launch")
         hw_flops = (pmc.get("k_solve_sq") or {}).get("hw_fp64_flops_per_launch")
-        metric = BASELINE_METRIC if (args.config, N, B) == ("config3", 20, 4096) else \
-            f"MPC QP solves/s (horizon={N}, batch={B} per GPU)"
+        metric = BASELINE_METRIC if (args.config, N, per_gpu, strong) == ("config3", 20, 4096, False) else \
+            f"MPC QP solves/s (horizon={N}, {'global batch' if strong else 'batch per GPU'}={total if strong else per_gpu})"
         out = {
             "metric": metric,
             "value": value,
@@ -273,28 +464,28 @@ def main() -> int:
             "warmup": args.warmup,
             "ms_per_step": ms_per_step,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if strong else "weak",
             "vs_baseline": None,
             "dtype": "f64",
-            "data": "synthetic: BASELINE config 3 inputs derived from the reference's default RRT* tree "
+            "data": "synthetic: BASELINE config inputs derived from the reference's default RRT* tree "
                     "(tests/golden/gen_golden.py), no external dataset",
             "config": {
                 "workload": name,
                 "config": args.config,
                 "batch_per_gpu": B,
-                "global_batch": B * world,
+                "global_batch": total,
                 "horizon": N,
                 "nx": 4,
                 "nu": 2,
                 "method": "admm+polish (OSQP algorithm, reference settings)" if args.method == "admm"
                 else "newton (polish only)",
-                "parallelism": f"dp{world} (independent shards)",
+                "parallelism": f"dp{world} (independent contiguous shards, {'strong' if strong else 'weak'})",
             },
-            "solved_fraction": solved_all / (B * world),
-            "iters_mean": {"admm": admm_all / (B * world), "polish": pol_all / (B * world)},
-            "kernel_ms": {"k_build": k1_ms, "k_solve": k2_ms},
+            "solved_fraction": solved_all / total,
+            "iters_mean": {"admm": admm_all / total, "polish": pol_all / total},
+            "kernel_ms": {"mpcqp_build": k1_ms, "k_solve": k2_ms},
             "roofline": {
-                "bound": "mfma",
+                "bound": "fp64_valu",
                 "achieved": achieved_tf,
                 "peak": FP64_PEAK_TFLOPS,
                 "unit": "TFLOP/s",
@@ -304,9 +495,10 @@ def main() -> int:
                 # the hardware's own count (SQ_INSTS_VALU_FLOPS_FP64, committed PMC pass) over this launch time
                 "hw_flops_per_launch": hw_flops,
                 "hw_frac": hw_flops / (k2_ms * 1e-3) / 1e12 / FP64_PEAK_TFLOPS if hw_flops else None,
-                "note": "FP64 compute roof (MI355X FP64 vector peak == FP64 matrix peak); k_solve is a "
-                        "latency-bound FP64 VALU kernel. Flops = bench.qp_flops (as implemented, counted "
-                        "per QP from the kernel's iteration counters) / mean k_solve event time.",
+                "note": "FP64 VALU roof (MI355X FP64 vector peak 78.6 TF; no MFMA is issued: f64 MFMA has "
+                        "the same peak and the per-QP matrices are <= 62x62). k_solve is a latency-bound "
+                        "FP64 VALU kernel. Flops = bench.qp_flops (as implemented, counted per QP from the "
+                        "kernel's iteration counters) / mean k_solve event time on the launch stream.",
             },
             "hbm_roofline": {
                 "achieved": hbm_gbs,
@@ -314,16 +506,24 @@ def main() -> int:
                 "unit": "GB/s",
                 "frac": hbm_gbs / HBM_PEAK_GBS,
                 "bytes_per_qp": qp_bytes(N),
-                "note": "compulsory f64 I/O per QP over the whole step (K1+K2); not the binding roof",
+                "note": "compulsory f64 I/O per QP over the whole step; not the binding roof",
             },
         }
+        # checker leg: the gathered global result against the C restatement on a strided sample
+        if args.check_sample > 0:
+            idx = np.unique(np.linspace(0, total - 1, min(total, args.check_sample)).astype(int))
+            out["rel_err"] = spot_check(params, batch.x0, batch.ref, batch.u_prev, g["U"], g["active"],
+                                        g["status"], idx)
+            out["rel_err"]["gathered_qps"] = int(len(g["status"]))
+            out["rel_err"]["gathered_solved"] = int((g["status"] == 1).sum())
         if world == 1 and args.cpu_seconds > 0:
-            out["rel_err"], out["cpu_baseline"] = cpu_baseline(
-                params, x0, ref, u_prev, args.cpu_seconds, ctrl._U[:B].cpu().numpy(), ctrl._active[:B].cpu().numpy())
+            out["cpu_baseline"] = cpu_baseline(params, x0, ref, u_prev, args.cpu_seconds)
+        if world == 1 and not args.no_config1:
+            out["config1"] = config1_closed_loop()
         print(json.dumps(out), flush=True)
+    ctx.barrier()
     ctrl.close()
-    if world > 1:
-        dist.destroy_process_group()
+    ctx.close()
     return 0
 
 

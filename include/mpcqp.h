@@ -187,7 +187,9 @@ typedef struct mpcqp_fleet {
   double* u_trace;           /* V x max_steps x 2: applied input of each step (nullable) */
 } mpcqp_fleet;
 
-/* One closed-loop step for every RUNNING vehicle.  `nominal` holds the base parameters,
+/* One closed-loop step for every RUNNING vehicle.  The device validates each RUNNING vehicle's
+ * loop state before any indexed access: ref_len outside [1, ref_stride] or path_idx < 0 ->
+ * MPCQP_FLEET_ABORTED, steps outside [0, max_steps) -> MPCQP_FLEET_OUT_OF_STEPS.  `nominal` holds the base parameters,
  * `relaxed` the retry parameters of control_stage.py:45-55 (du_bounds widened by
  * (5, 0.05); the reference speed column is scaled by 0.6 on the device); both have the
  * same horizon and max_batch >= V.  Vehicles not RUNNING are skipped (their waves exit). */

@@ -1,17 +1,16 @@
-// mpcqp.hip -- MI355X (gfx950) batched bicycle-MPC QP solver: kernels + C-ABI.
+// mpcqp.hip -- MI355X (gfx950) batched bicycle-MPC QP solver: the C-ABI, K1 and the launcher table.
 //
 // Replaces the reference's per-step MPC solve (CagriCatik/RRT-MPC):
-//   K1  k_build  : window -> LTV model      (src/control/mpc_controller.py:59-70,108,
+//   K1 k_build     window -> LTV model      (src/control/mpc_controller.py:59-70,108,
 //                                            src/control/vehicle_model.py:24-45)
-//   K2a k_setup  : condense + Ruiz scaling   (mpc_controller.py:53-117 -> OSQP setup)
-//   K2b k_admm   : OSQP ADMM iterations      (mpc_controller.py:119-132, settings :121-131)
-//   K2c k_finish : polish + outputs/status   (OSQP polish; mpc_controller.py:133-141)
-// One 64-lane wavefront owns one QP (B QPs -> B single-wave workgroups).  Every
-// vector of the iteration is distributed one decision variable per lane; the
-// structured constraint operators are DPP wave scans; the KKT inverse lives one
-// row per lane in registers.  The phases are separate kernels so that each gets
-// its own register budget (occupancy); the per-QP solver state between them
-// (scaled Hessian + scaling vectors, ~20 KB at N=20) stays L2/MALL resident.
+//   K2 k_solve<N>  ONE fused kernel per horizon (mpcqp_solve.h): setup (condensing + OSQP Ruiz
+//                  scaling, mpc_controller.py:53-117), ADMM (OSQP's iteration with the settings
+//                  of :119-132), polish + outputs/status (:133-141), with no kernel boundary in
+//                  between.
+// One 64-lane wavefront owns one QP (B QPs -> B single-wave workgroups).  Vectors are distributed
+// one decision variable per lane; the banded constraint operators are DPP lane shifts; the KKT
+// inverse lives one row per lane in registers and the scaled Hessian in LDS, so the scaled
+// problem never leaves the CU (the per-QP state buffer is written only with debug_state).
 // The algorithm is restated sequentially in oracle/mpcqp_cpu.c -- see DESIGN.md.
 #include "mpcqp_build.h"
 #ifdef MPCQP_ONLY_N

@@ -29,6 +29,16 @@ __global__ __launch_bounds__(kWave) void k_fleet_build(mpcqp_params p, mpcqp_fle
     go = f.mask[b] && !(st == MPCQP_SOLVED || st == MPCQP_SOLVED_INACCURATE);
   } else {
     go = f.phase[b] == MPCQP_FLEET_RUNNING;
+    // device-side validation of the loop state a C-ABI caller hands over (check_fleet cannot see
+    // device data): an unusable reference aborts the vehicle, a full trace ends its run -- before
+    // any indexed access
+    const int len0 = f.ref_len[b], pi0 = f.path_idx[b], st0 = f.steps[b];
+    const bool bad_ref = len0 < 1 || len0 > f.ref_stride || pi0 < 0;
+    const bool full = st0 < 0 || st0 >= f.max_steps;
+    if (go && (bad_ref || full)) {
+      if (lane == 0) f.phase[b] = bad_ref ? MPCQP_FLEET_ABORTED : MPCQP_FLEET_OUT_OF_STEPS;
+      go = false;
+    }
   }
   if (lane == 0) f.mask[(size_t)relax * V + b] = go ? 1 : 0;
   if (!go) return;
@@ -80,6 +90,10 @@ __global__ __launch_bounds__(kWave) void k_fleet_advance(double dt, double L, mp
   for (int i = 0; i < 4; ++i) x[i] = f.state[(size_t)b * 4 + i];
   plant(x, a, delta, dt, L, xn);
   const int k = f.steps[b];
+  if (k < 0 || k >= f.max_steps) {  // k_fleet_build already ended such a run; never write past the trace
+    f.phase[b] = MPCQP_FLEET_OUT_OF_STEPS;
+    return;
+  }
   for (int i = 0; i < 4; ++i) f.state[(size_t)b * 4 + i] = xn[i];
   if (f.trace)
     for (int i = 0; i < 4; ++i) f.trace[((size_t)b * f.max_steps + k) * 4 + i] = xn[i];

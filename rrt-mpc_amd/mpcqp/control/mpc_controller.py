@@ -142,6 +142,8 @@ class BatchedMPCController:
         if B > self.max_batch:
             raise ValueError(f"batch {B} exceeds max_batch {self.max_batch}")
         x0_t = self._device_input(x0, (B, 4), "x0")
+        if len(ref.shape) == 3 and ref.shape[1] > N + 1:  # rows past N are never read (see solve)
+            ref = ref[:, : N + 1]
         ref_t = self._device_input(ref, (B, N + 1, 4), "ref")
         up_t = None if u_prev is None else self._device_input(u_prev, (B, 2), "u_prev")
         if stream is None:
@@ -188,8 +190,11 @@ def _single_controller(params, method: str = "admm", **settings) -> BatchedMPCCo
 class MPCController:
     """Quadratic-cost MPC controller with soft bounds and rate limits (``mpc_controller.py:33-145``)."""
 
-    def __init__(self, params: MPCParameters) -> None:
+    def __init__(self, params: MPCParameters, **settings) -> None:
+        # ``settings``: optional solver settings of ``mpcqp_params`` (rho, max_iter, polish, ...);
+        # the reference's constructor takes ``params`` alone and so does every caller of it.
         self._params = params
+        self._settings = dict(settings)
 
     def solve(
         self,
@@ -203,10 +208,14 @@ class MPCController:
         N = int(self._params.horizon)
         x0 = np.asarray(x0, dtype=float).reshape(1, 4)
         ref = np.asarray(ref_traj, dtype=float)
-        if ref.shape != (N + 1, 4):
-            raise ValueError(f"ref_traj must have shape {(N + 1, 4)}, got {ref.shape}")
+        # The reference reads rows 0..N of ref_traj (mpc_controller.py:68,111) after unwrapping
+        # the whole yaw column (:59-60); np.unwrap is a prefix operation, so the first N+1 rows
+        # unwrap identically on their own.  Fewer rows fail there (ref[N]) and here.
+        if ref.ndim != 2 or ref.shape[1] != 4 or ref.shape[0] < N + 1:
+            raise ValueError(f"ref_traj must have shape (>= {N + 1}, 4), got {ref.shape}")
+        ref = ref[: N + 1]
         up = np.zeros((1, 2)) if u_prev is None else np.asarray(u_prev, dtype=float).reshape(1, 2)
-        ctrl = _single_controller(self._params)
+        ctrl = _single_controller(self._params, **self._settings)
         sol = ctrl.solve_batch(x0, ref[None], up)
         status = int(sol.status.cpu()[0])
         if status == _lib.NUMERICAL_ERROR:

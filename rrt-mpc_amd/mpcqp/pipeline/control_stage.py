@@ -57,6 +57,10 @@ class TrajectoryTracker:
 
     mpc: Any  # MPCConfig (reference or mpcqp.config)
     viz: Any  # VizConfig
+    # Optional solver settings (mpcqp_params names) of the nominal and the relaxed solve; the
+    # reference constructs TrajectoryTracker(mpc, viz) and gets the library defaults.
+    solver_settings: dict = field(default_factory=dict)
+    relaxed_solver_settings: dict = field(default_factory=dict)
 
     def _solve_with_relaxation(
         self,
@@ -66,7 +70,7 @@ class TrajectoryTracker:
         base_params: MPCParameters,
     ) -> Tuple[Optional[np.ndarray], Optional[np.ndarray], Optional[np.ndarray]]:
         """``control_stage.py:33-56``: nominal solve, then one retry with relaxed rates and speed."""
-        controller = MPCController(base_params)
+        controller = MPCController(base_params, **self.solver_settings)
         u0, Xp, Up = controller.solve(state, reference, u_prev=u_prev)
         if u0 is not None:
             return u0, Xp, Up
@@ -80,7 +84,8 @@ class TrajectoryTracker:
                 (base_params.du_bounds[1][0] - 0.05, base_params.du_bounds[1][1] + 0.05),
             ),
         )
-        return MPCController(relaxed_params).solve(state, relaxed_reference, u_prev=u_prev)
+        return MPCController(relaxed_params, **self.relaxed_solver_settings).solve(
+            state, relaxed_reference, u_prev=u_prev)
 
     def step(
         self,

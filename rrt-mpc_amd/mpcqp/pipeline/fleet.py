@@ -72,7 +72,8 @@ class FleetTracker:
     """
 
     def __init__(self, mpc, *, map_resolution: float, max_vehicles: int, max_ref_len: int,
-                 device=None, use_graph: bool = True, **settings) -> None:
+                 device=None, use_graph: bool = True, relaxed_settings: Optional[dict] = None,
+                 **settings) -> None:
         import torch
 
         from ..control.mpc_controller import BatchedMPCController
@@ -85,8 +86,11 @@ class FleetTracker:
         self.max_ref_len = int(max_ref_len)
         self.use_graph = bool(use_graph)
         self._nominal = BatchedMPCController(self.params, self.max_vehicles, device=device, **settings)
+        # the retry's solver settings default to the nominal ones (control_stage.py:50-56 changes
+        # only du_bounds and the reference speed)
+        rs = settings if relaxed_settings is None else relaxed_settings
         self._relaxed = BatchedMPCController(relaxed_parameters(self.params), self.max_vehicles,
-                                             device=self._nominal.device, **settings)
+                                             device=self._nominal.device, **rs)
         self.device = self._nominal.device
         self._L = _lib.lib()
         self._bufs = None

@@ -12,6 +12,7 @@ post-processing, restated below.
 """
 from __future__ import annotations
 
+import copy
 import ctypes
 import logging
 import math
@@ -76,11 +77,12 @@ class PlanResult:
     smoothed_path: Optional[Sequence[Tuple[float, float]]] = None
 
 
-def draw_samples(seed: int, goal, shape, goal_sample_rate: float, max_iterations: int) -> np.ndarray:
-    """The planner's sample of every iteration (``_sample``, ``rrt_star.py:320-325``): the same
+def draw_samples(seed, goal, shape, goal_sample_rate: float, max_iterations: int) -> np.ndarray:
+    """The planner's sample of every iteration (``_sample``, ``rrt_star.py:296-301``): the same
     ``numpy.random.default_rng(seed)`` calls in the same order (one per iteration, whether or
-    not the iteration then adds a node)."""
-    rng = np.random.default_rng(seed)
+    not the iteration then adds a node).  ``seed`` may also be a live ``numpy.random.Generator``,
+    which is advanced by the draws."""
+    rng = seed if isinstance(seed, np.random.Generator) else np.random.default_rng(seed)
     out = np.empty((max_iterations, 2))
     h, w = int(shape[0]), int(shape[1])
     gx, gy = float(goal[0]), float(goal[1])
@@ -206,11 +208,12 @@ class BatchedRRTStarPlanner:
         c.height, c.width = (int(v) for v in self.occupancy.shape)
         self._c = c
 
-    def grow(self, starts, goals, seeds, stream=None, *, host_samples: bool = False):
+    def grow(self, starts, goals, seeds, stream=None, *, host_samples: bool = False, samples=None):
         """Launch the tree growth; returns device tensors (nodes (V, M, 4), count (V,), meta (V, 2)).
 
         The samples replay ``numpy.random.default_rng(seed)``: drawn on the device from the
-        generator's PCG64 state (default), or with ``host_samples=True`` by numpy itself."""
+        generator's PCG64 state (default), or with ``host_samples=True`` by numpy itself, or
+        given as ``samples`` (V, max_iterations, 2)."""
         torch = self._torch
         starts = np.asarray(starts, dtype=float).reshape(-1, 2)
         goals = np.asarray(goals, dtype=float).reshape(-1, 2)
@@ -219,7 +222,9 @@ class BatchedRRTStarPlanner:
         dev = self.device
         sg = torch.from_numpy(np.hstack([starts, goals]) if V else np.zeros((1, 4))).to(dev)
         smp = rs = None
-        if host_samples:
+        if samples is not None:
+            smp = torch.from_numpy(np.ascontiguousarray(samples, dtype=np.float64).reshape(V, T, 2)).to(dev)
+        elif host_samples:
             samples = np.stack([draw_samples(int(s), g, self.occupancy.shape, self.params.goal_sample_rate, T)
                                 for s, g in zip(seeds, goals)]) if V else np.zeros((1, T, 2))
             smp = torch.from_numpy(samples).to(dev)
@@ -289,13 +294,14 @@ class BatchedRRTStarPlanner:
             out.append(working)
         return out
 
-    def plan_batch(self, starts, goals, seeds=None) -> List[PlanResult]:
-        """``plan(start, goal)`` for every problem (seed defaults to ``params.random_seed``)."""
+    def plan_batch(self, starts, goals, seeds=None, *, samples=None) -> List[PlanResult]:
+        """``plan(start, goal)`` for every problem (seed defaults to ``params.random_seed``;
+        ``samples`` (V, max_iterations, 2) replaces the seeds' streams)."""
         starts = np.asarray(starts, dtype=float).reshape(-1, 2)
         V = len(starts)
         if seeds is None:
             seeds = [self.params.random_seed] * V
-        nodes, count, meta = self.grow(starts, goals, seeds)
+        nodes, count, meta = self.grow(starts, goals, seeds, samples=samples)
         nodes = nodes.cpu().numpy()
         count = count.cpu().numpy()
         meta = meta.cpu().numpy()
@@ -315,11 +321,24 @@ class RRTStarPlanner:
     def __init__(self, occupancy: np.ndarray, params: PlannerParameters) -> None:
         self.occupancy = occupancy
         self.params = params
+        # one generator per planner, advanced across plan() calls (rrt_star.py:199,296-301)
+        self.rng = np.random.default_rng(params.random_seed)
+        self._batched = None
 
     def plan(self, start: Tuple[float, float], goal: Tuple[float, float]) -> PlanResult:
         LOG.info("Running RRT* planner from %s to %s (max_iterations=%d)", start, goal, self.params.max_iterations)
-        planner = BatchedRRTStarPlanner(self.occupancy, self.params)
-        return planner.plan_batch([start], [goal], [self.params.random_seed])[0]
+        if self._batched is None:
+            self._batched = BatchedRRTStarPlanner(self.occupancy, self.params)
+        T = int(self.params.max_iterations)
+        shape = np.asarray(self.occupancy).shape
+        before = copy.deepcopy(self.rng.bit_generator.state)
+        samples = draw_samples(self.rng, goal, shape, self.params.goal_sample_rate, T)
+        result = self._batched.plan_batch([start], [goal], samples=samples[None])[0]
+        # the reference draws one sample per iteration it runs (the loop breaks at the goal):
+        # rewind and consume exactly that many, so the next plan() continues the same stream
+        self.rng.bit_generator.state = before
+        draw_samples(self.rng, goal, shape, self.params.goal_sample_rate, int(result.iterations))
+        return result
 
 
 __all__ = ["PlannerParameters", "RRTStarNode", "PlanResult", "RRTStarPlanner", "BatchedRRTStarPlanner",

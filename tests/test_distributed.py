@@ -1,9 +1,10 @@
-"""Multi-process (gloo, world_size 2) tests of the data-parallel path on CPU.
+"""Multi-process (gloo) tests of bench.py's data-parallel path on CPU.
 
-The batch shards contiguously over ranks with no data-path collective (bench.py); the only
-collectives are the timing MAX and the statistics SUM.  Here each rank solves its shard with
-the C restatement (no GPU in this container) and the gathered result must equal the
-single-process solve exactly.
+The ranks drive bench.py's own distributed functions -- ``shard_bounds``, ``DistContext``,
+``timed_steps``, ``reduce_stats``, ``gather_rows``, ``spot_check`` -- with the C restatement
+standing in for the GPU shard solve (there is no GPU in this container).  Weak scaling (per-rank
+batch) and strong scaling (a fixed global batch, including one that does not divide evenly) must
+both reproduce the single-process solve exactly.
 """
 from __future__ import annotations
 
@@ -25,7 +26,7 @@ def _free_port() -> int:
         return s.getsockname()[1]
 
 
-def _worker(rank, world, port, per_rank, out_dir):
+def _worker(rank, world, port, total, out_dir):
     for p in (ROOT / "rrt-mpc_amd", ROOT / "oracle", ROOT):
         sys.path.insert(0, str(p))
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
@@ -37,40 +38,68 @@ def _worker(rank, world, port, per_rank, out_dir):
     import mpc_oracle as mo
 
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    x0, ref, up, N, _ = bench.make_batch("config3", per_rank, world, rank)
-    out = cpu_solver.cpu_solve(mo.default_params(N), x0, ref, up, nthreads=2)
-    t = torch.tensor([float(rank + 1)], dtype=torch.float64)
-    dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    solved = torch.tensor([float((out["status"] == 1).sum())], dtype=torch.float64)
-    dist.all_reduce(solved, op=dist.ReduceOp.SUM)
-    gathered = [torch.zeros(per_rank, 2, dtype=torch.float64) for _ in range(world)]
-    dist.all_gather(gathered, torch.from_numpy(out["u0"]))
+    ctx = bench.DistContext(world, rank, rank, "gloo", torch.device("cpu"))
+    batch = bench.make_global_batch("config3", total)
+    lo, hi = bench.shard_bounds(total, world, rank)
+    counts = bench.shard_counts(total, world)
+    params = mo.default_params(batch.horizon)
+    res = {}
+
+    def step(k):
+        res.update(cpu_solver.cpu_solve(params, batch.x0[lo:hi], batch.ref[lo:hi], batch.u_prev[lo:hi], nthreads=1))
+
+    elapsed = bench.timed_steps(step, 2, 1, ctx)
+    T, (solved,) = bench.reduce_stats(ctx, elapsed + rank, [float((res["status"] == 1).sum())])
+    g = {k: bench.gather_rows(ctx, torch.from_numpy(res[k]), counts).numpy() for k in ("u0", "status", "U", "active")}
     if rank == 0:
-        np.savez(Path(out_dir) / "dist.npz", tmax=t.numpy(), solved=solved.numpy(),
-                 u0=torch.cat(gathered).numpy())
-    dist.barrier()
-    dist.destroy_process_group()
+        chk = bench.spot_check(params, batch.x0, batch.ref, batch.u_prev, g["U"], g["active"], g["status"],
+                               np.arange(0, total, 5))
+        np.savez(Path(out_dir) / "dist.npz", T=T, elapsed=elapsed, solved=solved, u0=g["u0"], status=g["status"],
+                 U=g["U"], err=chk["max_rel_err_U"], mism=chk["active_set_mismatches"] + chk["status_mismatches"])
+    ctx.barrier()
+    ctx.close()
 
 
 @pytest.mark.timeout(300)
-def test_two_rank_sharded_solve_matches_single_process(tmp_path):
+@pytest.mark.parametrize("world,total", [(2, 96), (3, 71)])
+def test_sharded_solve_matches_single_process(tmp_path, world, total):
+    """world ranks over gloo: contiguous shards (71 over 3 ranks: 24/24/23), MAX of time, SUM of
+    solved, all_gather of u0/status/U in rank order == the single-process solve bit for bit."""
     sys.path.insert(0, str(ROOT))
+    sys.path.insert(0, str(ROOT / "oracle"))
     import bench
     import cpu_solver
     import mpc_oracle as mo
 
-    world, per_rank = 2, 48
-    mp.start_processes(_worker, args=(world, _free_port(), per_rank, str(tmp_path)), nprocs=world,
+    mp.start_processes(_worker, args=(world, _free_port(), total, str(tmp_path)), nprocs=world,
                        start_method="spawn", join=True)
     d = np.load(tmp_path / "dist.npz")
-    assert d["tmax"][0] == 2.0
-    assert d["solved"][0] == world * per_rank
-    x0, ref, up, N, _ = bench.make_batch("config3", per_rank * world, 1, 0)
-    full = cpu_solver.cpu_solve(mo.default_params(N), x0, ref, up, nthreads=2)
+    # MAX over ranks: rank r reported its elapsed time + r seconds
+    assert float(d["T"]) >= max(float(d["elapsed"]), world - 1.0)
+    assert float(d["solved"]) == total
+    b = bench.make_global_batch("config3", total)
+    full = cpu_solver.cpu_solve(mo.default_params(b.horizon), b.x0, b.ref, b.u_prev, nthreads=2)
     np.testing.assert_array_equal(d["u0"], full["u0"])
+    np.testing.assert_array_equal(d["U"], full["U"])
+    np.testing.assert_array_equal(d["status"], full["status"])
+    assert float(d["err"]) == 0.0 and int(d["mism"]) == 0
 
 
-def test_shards_are_contiguous_and_cover_the_batch():
+def test_shard_bounds_cover_any_total():
+    sys.path.insert(0, str(ROOT))
+    import bench
+
+    for total in (0, 1, 7, 16384, 16385):
+        for world in (1, 2, 3, 8):
+            b = [bench.shard_bounds(total, world, r) for r in range(world)]
+            assert b[0][0] == 0 and b[-1][1] == total
+            assert all(b[r][1] == b[r + 1][0] for r in range(world - 1))
+            sizes = [hi - lo for lo, hi in b]
+            assert max(sizes) - min(sizes) <= 1
+            assert sizes == bench.shard_counts(total, world)
+
+
+def test_weak_shards_are_contiguous_and_cover_the_batch():
     sys.path.insert(0, str(ROOT))
     import bench
 
