@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define MPCQP_ABI_VERSION 3
+#define MPCQP_ABI_VERSION 4
 
 /* error codes (function return values) */
 #define MPCQP_OK 0
@@ -45,7 +45,9 @@ extern "C" {
 #define MPCQP_E_HIP (-4)         /* HIP runtime / launch error */
 #define MPCQP_E_STATE (-5)       /* mpcqp_solve before mpcqp_build of the same B */
 
-#define MPCQP_MAX_HORIZON 31     /* 2N+1 <= 64: one QP per 64-lane wavefront */
+#define MPCQP_MAX_HORIZON 63     /* N+1 <= 64: K1 builds a window on one 64-lane wavefront */
+#define MPCQP_WIDE_MIN_HORIZON 32 /* N <= 31: one wave per QP (2N variables on the lanes, the KKT
+                                     inverse in registers); N >= 32: one 256-thread workgroup per QP */
 
 /* per-QP status codes (mirror OSQP's; mpc_controller.py:137 accepts 1 and 2) */
 #define MPCQP_SOLVED 1            /* polish converged: exact optimum (active set reproduces itself) */

@@ -142,6 +142,39 @@ def cpu_solve(params, x0, ref, u_prev=None, *, method: int = 0, nthreads: int = 
     return out
 
 
+def cpu_solve_models(params, models, *, method: int = 0, nthreads: int = 0, **solver):
+    """The solve from given LTV models (B, mpcqp_model_stride(N)) -- e.g. the GPU's K1 output, so
+    the device/glibc sin/cos ulps stay out of an iteration-count comparison."""
+    L = lib()
+    if not hasattr(L, "_models_bound"):
+        dp = ctypes.POINTER(ctypes.c_double)
+        ip = ctypes.POINTER(ctypes.c_int32)
+        bp = ctypes.POINTER(ctypes.c_uint8)
+        L.mpcqp_cpu_solve_models.argtypes = [ctypes.POINTER(CParams), ctypes.c_int, dp, dp, dp, dp, ip, ip, bp,
+                                             ctypes.c_int]
+        L.mpcqp_cpu_solve_models.restype = ctypes.c_int
+        L._models_bound = True
+    cp = make_cparams(params, method, **solver)
+    N = cp.horizon
+    models = np.ascontiguousarray(models, dtype=np.float64)
+    B = models.shape[0]
+    out = dict(
+        u0=np.zeros((B, 2)),
+        X=np.zeros((B, 4, N + 1)),
+        U=np.zeros((B, 2, N)),
+        status=np.zeros(B, np.int32),
+        iters=np.zeros((B, 4), np.int32),
+        active=np.zeros((B, 5 * N + 1), np.uint8),
+    )
+    dp = ctypes.c_double
+    rc = L.mpcqp_cpu_solve_models(ctypes.byref(cp), B, _p(models, dp), _p(out["u0"], dp), _p(out["X"], dp),
+                                  _p(out["U"], dp), _p(out["status"], ctypes.c_int32), _p(out["iters"], ctypes.c_int32),
+                                  _p(out["active"], ctypes.c_uint8), int(nthreads if nthreads else (os.cpu_count() or 1)))
+    if rc != 0:
+        raise RuntimeError(f"mpcqp_cpu_solve_models failed: {rc}")
+    return out
+
+
 def cpu_state(params, model: np.ndarray, state_stride: int, **solver) -> np.ndarray:
     """Scaled QP (GPU state layout) for each model row: (B, state_stride)."""
     L = lib()
@@ -158,4 +191,4 @@ def cpu_state(params, model: np.ndarray, state_stride: int, **solver) -> np.ndar
     return out
 
 
-__all__ = ["CParams", "make_cparams", "cpu_solve", "cpu_state", "build_library", "lib"]
+__all__ = ["CParams", "make_cparams", "cpu_solve", "cpu_solve_models", "cpu_state", "build_library", "lib"]

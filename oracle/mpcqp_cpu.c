@@ -612,7 +612,7 @@ void mpcqp_cpu_solve_one(const mpcqp_params* p, const double* model, double* u0,
   double x[MAXNV], z[MAXR], y[MAXR];
   for (int i = 0; i < n; ++i) x[i] = 0.0;
   for (int r = 0; r < m; ++r) z[r] = y[r] = 0.0;
-  int admm_ok = 0, bad = 0, polished = 0;
+  int admm_ok = 0, bad = 0, polished = 0, approx = 0;
   /* non-finite problem data (NaN/inf in x0, ref, u_prev) -> numerical error, as k_setup */
   for (int i = 0; i < n && !bad; ++i) {
     if (!isfinite(s->q[i])) bad = 1;
@@ -700,6 +700,12 @@ void mpcqp_cpu_solve_one(const mpcqp_params* p, const double* model, double* u0,
           admm_ok = 1;
           break;
         }
+        /* OSQP at max_iter: eps_abs and eps_rel x10 -> solved_inaccurate, no polish */
+        if (it == p->max_iter) {
+          approx = pr <= 10.0 * p->eps_abs + 10.0 * p->eps_rel * fmax(nAx, nz) &&
+                   du <= 10.0 * p->eps_abs + 10.0 * p->eps_rel * fmax(fmax(nPx, nAty), nq) * ic;
+          break;
+        }
         /* early polish: an exact optimum found now satisfies the termination test itself */
         /* ... from polish_from on, or earlier once both residuals are near their tolerances */
         const int near = p->polish_near > 0.0 && it >= 2 * p->check_termination &&
@@ -730,11 +736,12 @@ void mpcqp_cpu_solve_one(const mpcqp_params* p, const double* model, double* u0,
         }
       }
     }
-    st = admm_ok ? MPCQP_SOLVED : MPCQP_MAX_ITER_REACHED;
+    st = admm_ok ? MPCQP_SOLVED : (approx ? MPCQP_SOLVED_INACCURATE : MPCQP_MAX_ITER_REACHED);
   }
 
   /* ---- polish after ADMM (first guess: the ADMM z iterate), or from x = 0 (method newton) ---- */
-  const int do_polish = ((p->method == MPCQP_METHOD_NEWTON) || p->polish) && !polished;
+  /* OSQP polishes only a solved ADMM run; method newton is the polish alone */
+  const int do_polish = p->method == MPCQP_METHOD_NEWTON ? 1 : (p->polish && admm_ok);
   double xa[MAXNV];
   memcpy(xa, x, sizeof(double) * n);
   if (polished) {
@@ -807,6 +814,27 @@ void mpcqp_cpu_solve_one(const mpcqp_params* p, const double* model, double* u0,
     iters[2] = n_fact;
     iters[3] = n_ls;
   }
+}
+
+/* The solve of B QPs from given LTV models (B x mpcqp_model_stride(N), e.g. the GPU's K1
+ * output): the iteration-count checks feed the device's model so the transcendental ulps of
+ * sin/cos (device vs glibc) stay out of the comparison. */
+int mpcqp_cpu_solve_models(const mpcqp_params* p, int B, const double* models, double* u0, double* X, double* U,
+                           int32_t* status, int32_t* iters, uint8_t* active, int nthreads) {
+  if (!p || B < 0 || !models) return MPCQP_E_ARG;
+  const int N = p->horizon;
+  if (N < 1 || N > MAXN) return MPCQP_E_HORIZON;
+  const int S = mpcqp_model_stride(N);
+#ifdef _OPENMP
+  if (nthreads > 0) omp_set_num_threads(nthreads);
+#pragma omp parallel for schedule(dynamic, 4)
+#endif
+  for (int b = 0; b < B; ++b)
+    mpcqp_cpu_solve_one(p, models + (size_t)S * b, u0 ? u0 + 2 * (size_t)b : NULL,
+                        X ? X + 4 * (size_t)(N + 1) * b : NULL, U ? U + 2 * (size_t)N * b : NULL,
+                        status ? status + b : NULL, iters ? iters + 4 * (size_t)b : NULL,
+                        active ? active + (size_t)(5 * N + 1) * b : NULL);
+  return MPCQP_OK;
 }
 
 /* Same contract as mpcqp_build + mpcqp_solve on HOST pointers, OpenMP over the batch. */

@@ -67,12 +67,18 @@ __global__ __launch_bounds__(kWave) void k_wave_ops(const double* __restrict__ i
 #else
 #define MPCQP_L(N) &mpcqp::launch_solve<N>
 #endif
-const mpcqp::launcher_t kLaunchers[MPCQP_MAX_HORIZON + 1] = {
+const mpcqp::launcher_t kLaunchers[MPCQP_WIDE_MIN_HORIZON] = {
     nullptr,     MPCQP_L(1),  MPCQP_L(2),  MPCQP_L(3),  MPCQP_L(4),  MPCQP_L(5),  MPCQP_L(6),  MPCQP_L(7),
     MPCQP_L(8),  MPCQP_L(9),  MPCQP_L(10), MPCQP_L(11), MPCQP_L(12), MPCQP_L(13), MPCQP_L(14), MPCQP_L(15),
     MPCQP_L(16), MPCQP_L(17), MPCQP_L(18), MPCQP_L(19), MPCQP_L(20), MPCQP_L(21), MPCQP_L(22), MPCQP_L(23),
     MPCQP_L(24), MPCQP_L(25), MPCQP_L(26), MPCQP_L(27), MPCQP_L(28), MPCQP_L(29), MPCQP_L(30), MPCQP_L(31)};
 #undef MPCQP_L
+
+// per-QP doubles of the solver state buffer (debug state of the one-wave kernel, the workspace
+// of the long-horizon kernel)
+size_t ws_state_stride(int N) {
+  return N >= MPCQP_WIDE_MIN_HORIZON ? mpcqp::wide_stride(N) : (size_t)state_stride(N);
+}
 
 thread_local std::string g_err;
 using mpcqp::fail;
@@ -80,8 +86,9 @@ using mpcqp::fail;
 int check_params(const mpcqp_params* p) {
   if (!p) return fail(MPCQP_E_ARG, "null params");
   if (p->horizon < 1 || p->horizon > MPCQP_MAX_HORIZON)
-    return fail(MPCQP_E_HORIZON, "horizon " + std::to_string(p->horizon) + " outside [1, 31]");
-  if (!kLaunchers[p->horizon]) return fail(MPCQP_E_HORIZON, "horizon not compiled into this build");
+    return fail(MPCQP_E_HORIZON, "horizon " + std::to_string(p->horizon) + " outside [1, " +
+                                     std::to_string(MPCQP_MAX_HORIZON) + "]");
+  if (!mpcqp::launcher(p->horizon)) return fail(MPCQP_E_HORIZON, "horizon not compiled into this build");
   if (!(p->dt > 0.0) || !(p->wheelbase_px > 0.0)) return fail(MPCQP_E_ARG, "dt and wheelbase_px must be > 0");
   if (p->method != MPCQP_METHOD_ADMM && p->method != MPCQP_METHOD_NEWTON) return fail(MPCQP_E_ARG, "bad method");
   if (p->max_iter < 1 || p->check_termination < 1 || p->adaptive_rho_interval < 1 || p->polish_max_iter < 0 ||
@@ -100,7 +107,8 @@ int fail(int code, const std::string& msg) {
   return code;
 }
 launcher_t launcher(int horizon) {
-  return horizon >= 1 && horizon <= MPCQP_MAX_HORIZON ? kLaunchers[horizon] : nullptr;
+  if (horizon >= MPCQP_WIDE_MIN_HORIZON && horizon <= MPCQP_MAX_HORIZON) return &launch_solve_wide;
+  return horizon >= 1 && horizon < MPCQP_WIDE_MIN_HORIZON ? kLaunchers[horizon] : nullptr;
 }
 }  // namespace mpcqp
 
@@ -131,7 +139,7 @@ int mpcqp_create(const mpcqp_params* p, int max_batch, int device, mpcqp_ws** ws
   w->model = nullptr;
   w->state = nullptr;
   const size_t mbytes = sizeof(double) * (size_t)model_stride(p->horizon) * (size_t)max_batch;
-  const size_t sbytes = sizeof(double) * (size_t)state_stride(p->horizon) * (size_t)max_batch;
+  const size_t sbytes = sizeof(double) * ws_state_stride(p->horizon) * (size_t)max_batch;
   e = hipMalloc(&w->model, mbytes);
   if (e == hipSuccess) e = hipMalloc(&w->state, sbytes);
   if (e != hipSuccess) {
@@ -180,7 +188,7 @@ int mpcqp_solve(mpcqp_ws* ws, int B, double* u0, double* X, double* U, int32_t* 
   if (B == 0) return MPCQP_OK;
   hipStream_t s = static_cast<hipStream_t>(stream);
   Launch L{&ws->p, B, ws->model, ws->state, u0, X, U, status, iters, active, nullptr};
-  kLaunchers[ws->p.horizon](s, L);
+  mpcqp::launcher(ws->p.horizon)(s, L);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return fail(MPCQP_E_HIP, std::string("k_solve launch: ") + hipGetErrorString(e));
   return MPCQP_OK;
@@ -190,7 +198,7 @@ const double* mpcqp_model_buffer(const mpcqp_ws* ws) { return ws ? ws->model : n
 
 const double* mpcqp_state_buffer(const mpcqp_ws* ws) { return ws ? ws->state : nullptr; }
 
-int mpcqp_state_stride(int horizon) { return state_stride(horizon); }
+int mpcqp_state_stride(int horizon) { return (int)ws_state_stride(horizon); }
 
 int mpcqp_debug_stamps(unsigned long long* out32, int reset) {
 #ifdef MPCQP_STAMPS

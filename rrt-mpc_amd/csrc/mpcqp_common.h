@@ -262,6 +262,10 @@ typedef void (*launcher_t)(hipStream_t, const Launch&);
 // mpcqp_part.hip objects (parallel build) or in mpcqp.hip itself (MPCQP_ONLY_N dev builds).
 template <int N>
 void launch_solve(hipStream_t s, const Launch& L);
+// the long-horizon solve (N >= MPCQP_WIDE_MIN_HORIZON; mpcqp_wide.hip): one 256-thread workgroup
+// per QP, L.state = its workspace (wide_stride(N) doubles per QP)
+void launch_solve_wide(hipStream_t s, const Launch& L);
+size_t wide_stride(int horizon);
 // launcher of horizon N (nullptr when not compiled in); defined in mpcqp.hip
 launcher_t launcher(int horizon);
 // records msg as mpcqp_last_error() of the calling thread and returns code; defined in mpcqp.hip

@@ -91,14 +91,41 @@ struct Ctx {
     return D * t;
   }
   // (Pbar v)_lane, Pbar symmetric: lane reads its row as a conflict-free column of the LDS copy
+  // The column loads go out in groups of kPG ahead of their FMAs (the inline-asm FMAs pin each
+  // load's register otherwise: one load + lgkmcnt(0) wait per column).
+  // Past N = 24 the 9 registers of the look-ahead would spill the inverse: plain loads there.
+  static constexpr int kPG = 4;
   __device__ __forceinline__ double Pmul(double v) const {
     double w[4];
     bcast<kNW>(act ? v : 0.0, w);
     const int col = act ? lane : 0;
     double a[4] = {0.0, 0.0, 0.0, 0.0};
-    Unroll<0, n>::run([&](auto jc) {
-      constexpr int j = decltype(jc)::value;
-      fmac_bc<j % 16>(a[j % 4], w[j / 16], P[j * n + col]);
+    if constexpr (N > 24) {
+      Unroll<0, n>::run([&](auto jc) {
+        constexpr int j = decltype(jc)::value;
+        fmac_bc<j % 16>(a[j % 4], w[j / 16], P[j * n + col]);
+      });
+      return act ? (a[0] + a[1]) + (a[2] + a[3]) : 0.0;
+    }
+    double cur[kPG], nxt[kPG];
+    Unroll<0, kPG>::run([&](auto kc) {
+      constexpr int k = decltype(kc)::value;
+      cur[k] = k < n ? P[k * n + col] : 0.0;
+    });
+    Unroll<0, (n + kPG - 1) / kPG>::run([&](auto gc) {
+      constexpr int g = decltype(gc)::value;
+      if constexpr ((g + 1) * kPG < n) {
+        Unroll<0, kPG>::run([&](auto kc) {
+          constexpr int j = (g + 1) * kPG + decltype(kc)::value;
+          nxt[decltype(kc)::value] = j < n ? P[j * n + col] : 0.0;
+        });
+      }
+      __builtin_amdgcn_sched_barrier(0);  // the next group's loads stay ahead of this group's FMAs
+      Unroll<0, kPG>::run([&](auto kc) {
+        constexpr int j = g * kPG + decltype(kc)::value;
+        if constexpr (j < n) fmac_bc<j % 16>(a[j % 4], w[j / 16], cur[decltype(kc)::value]);
+      });
+      Unroll<0, kPG>::run([&](auto kc) { cur[decltype(kc)::value] = nxt[decltype(kc)::value]; });
     });
     return act ? (a[0] + a[1]) + (a[2] + a[3]) : 0.0;
   }
@@ -117,6 +144,8 @@ struct Ctx {
     const double bp2 = D * shl2(D) * up2, bp4 = D * shl4(D) * up4;
     const double bm2 = shr2(bp2), bm4 = shr4(bp4);  // symmetric: (p, p-2) = lane p-2's (., +2)
     const int col = ln < n ? ln : 0;
+    const bool live = ln < n;
+    // every lane loads (lanes >= n read column 0 and discard it): no exec-masked load per column
     Unroll<0, n>::run([&](auto jc) {
       constexpr int j = decltype(jc)::value;
       double t = 0.0;
@@ -125,7 +154,8 @@ struct Ctx {
       if (j + 2 == ln) t = bm2;
       if (j == ln + 4) t = bp4;
       if (j + 4 == ln) t = bm4;
-      r[j] = ln < n ? P[j * n + col] + t : 0.0;
+      const double pv = P[j * n + col];
+      r[j] = live ? pv + t : 0.0;
     });
   }
   // Symmetric sweep operator on the rows in r[]: afterwards A^{-1} = -r (row `lane`).
@@ -400,12 +430,13 @@ __device__ __forceinline__ bool setup_qp(const mpcqp_params& p, int b, const dou
 
   // ---- unscaled data: P = 2H (column `lane`), q = 2g, folded row bounds ----
   double qv = act ? 2.0 * sm.g[lane] : 0.0;
-  double cmax = 0.0;  // running column max of |P|
+  double cmx[4] = {0.0, 0.0, 0.0, 0.0};  // column max of |P| (partial maxima)
 #pragma unroll
   for (int i = 0; i < n; ++i) {
     Pc[i] = 2.0 * Pc[i];
-    cmax = fmax(cmax, fabs(Pc[i]));
+    cmx[i % 4] = fmax(cmx[i % 4], fabs(Pc[i]));
   }
+  double cmax = fmax(fmax(cmx[0], cmx[1]), fmax(cmx[2], cmx[3]));
   double lo[3], hi[3], wt[3], E[3];
   // unscaled row coefficients (slot 1: own, 2 back; slot 2: own, 2 back, 4 back)
   const double idt = 1.0 / dt, v0 = x0[3];
@@ -466,13 +497,14 @@ __device__ __forceinline__ bool setup_qp(const mpcqp_params& p, int b, const dou
     sm.buf[lane] = dl;
     lds_sync();
     const double dlc = dl * cpend;
-    double cm2 = 0.0;
+    double cmp[4] = {0.0, 0.0, 0.0, 0.0};  // four partial maxima: no serial fmax chain (max is exact)
 #pragma unroll
     for (int i = 0; i < n; ++i) {
       const double t = Pc[i] * (sm.buf[i] * dlc);
       Pc[i] = t;
-      cm2 = fmax(cm2, fabs(t));
+      cmp[i % 4] = fmax(cmp[i % 4], fabs(t));
     }
+    const double cm2 = fmax(fmax(cmp[0], cmp[1]), fmax(cmp[2], cmp[3]));
     D *= dl;
     qv *= dl;
     E[0] *= el0;
@@ -741,7 +773,7 @@ __device__ __forceinline__ int polish_qp(Ctx<N>& C, double& x, const double zg[3
 // the reference settings).  From iteration polish_from on, a termination check that fails also
 // attempts the polish: an exact optimum found there satisfies the termination test itself.
 // Returns the ADMM flag (-1 numerical error, 0 not converged, 1 converged, 2 solved by an early
-// polish); x, z, the counters out.
+// polish, 3 max_iter reached within 10x the tolerances); x, z, the counters out.
 template <int N>
 __device__ __forceinline__ int admm_qp(const mpcqp_params& p, Ctx<N>& C, bool bad, double& x_out, double z_out[3],
                                        int& it_out, int& nfact_out, int& pol_it, int& n_ls, double* __restrict__ dbg) {
@@ -749,7 +781,7 @@ __device__ __forceinline__ int admm_qp(const mpcqp_params& p, Ctx<N>& C, bool ba
   double x = 0.0, z[3] = {0.0, 0.0, 0.0}, y[3] = {0.0, 0.0, 0.0};
   double rho = p.rho;
   const double sg = p.sigma, alpha = p.alpha;
-  bool ok = false, polished = false;
+  bool ok = false, polished = false, approx = false;
   int it = 0, nfact = 0;
   const bool early = p.polish != 0 && p.polish_from > 0;
   Stamps T, T2;
@@ -853,6 +885,11 @@ __device__ __forceinline__ int admm_qp(const mpcqp_params& p, Ctx<N>& C, bool ba
           ok = true;
           break;
         }
+        // OSQP at max_iter: the same test with eps_abs and eps_rel x10 passes -> solved_inaccurate
+        // (no polish); otherwise max_iter_reached
+        // (the loop ends by itself after this check)
+        approx = it == p.max_iter && pr <= 10.0 * p.eps_abs + 10.0 * p.eps_rel * nprim &&
+                 du <= 10.0 * p.eps_abs + 10.0 * p.eps_rel * ndual * ic;
         // ... from polish_from on, or earlier once both residuals are near their tolerances
         const bool near = p.polish_near > 0.0 && it >= 2 * p.check_termination &&
                           fmax(pr / ep, du / ed) < p.polish_near;
@@ -883,7 +920,7 @@ __device__ __forceinline__ int admm_qp(const mpcqp_params& p, Ctx<N>& C, bool ba
       }
     }
   }
-  const int flag = bad ? -1 : (polished ? 2 : (ok ? 1 : 0));
+  const int flag = bad ? -1 : (polished ? 2 : (ok ? 1 : (approx ? 3 : 0)));
   if (dbg) {
     dbg[state_lane_off(N) + kFx * kWave + threadIdx.x] = act ? x : 0.0;
     if (threadIdx.x == 0) {
@@ -916,7 +953,9 @@ __device__ __forceinline__ void finish_qp(const mpcqp_params& p, int b, const do
   const bool act = C.act;
   const bool use_admm = p.method == MPCQP_METHOD_ADMM;
   const bool polished = admm_flag == 2;  // exact optimum already found by an early polish
-  const bool do_polish = (!use_admm || p.polish != 0) && !polished;
+  const bool approx = admm_flag == 3;    // OSQP's solved_inaccurate at max_iter: not polished
+  // OSQP polishes only a solved ADMM run (status solved); method newton is the polish alone
+  const bool do_polish = use_admm ? (p.polish != 0 && admm_flag == 1) : true;
   bool bad = admm_flag < 0;  // non-finite data (setup) or ADMM numerical error
   const bool admm_ok = admm_flag == 1;
   double x = use_admm ? x_in : 0.0;
@@ -946,7 +985,8 @@ __device__ __forceinline__ void finish_qp(const mpcqp_params& p, int b, const do
     status = MPCQP_SOLVED;
   } else if (use_admm) {
     if (do_polish) x = x_admm;  // polish failed: return the ADMM iterate (OSQP behaviour)
-    status = admm_ok ? (do_polish ? MPCQP_SOLVED_INACCURATE : MPCQP_SOLVED) : MPCQP_MAX_ITER_REACHED;
+    status = admm_ok ? (do_polish ? MPCQP_SOLVED_INACCURATE : MPCQP_SOLVED)
+                     : (approx ? MPCQP_SOLVED_INACCURATE : MPCQP_MAX_ITER_REACHED);
   } else {
     status = MPCQP_MAX_ITER_REACHED;
   }

@@ -1,0 +1,939 @@
+// mpcqp_wide.hip -- the solve for long horizons (MPCQP_WIDE_MIN_HORIZON <= N <= MPCQP_MAX_HORIZON).
+//
+// The one-wave kernel (mpcqp_solve.h) keeps a QP's KKT inverse one row per lane in registers,
+// which caps it at 2N <= 62 decision variables.  The reference builds its QP for any horizon
+// (src/control/mpc_controller.py:47-57), so longer horizons take this kernel: one 256-thread
+// workgroup (four waves) per QP, runtime N, the same algorithm -- condensing, OSQP Ruiz/cost
+// scaling, ADMM with adaptive rho and OSQP's termination, the active-set polish -- with every
+// array in a per-QP arena: LDS when it fits (N <= ~50), else the workspace in HBM (then L2
+// resident); the scaled Hessian Pbar always lives in the workspace.
+//
+// Arithmetic: this kernel is oracle/mpcqp_cpu.c parallelised without changing a single floating
+// point operation -- elementwise work spread over the threads, every sum in the C code's
+// sequential order (thread 0 or the owning thread), maxima (exact) reduced in any order, no
+// contraction, IEEE division and square root.  Given the same LTV model (K1 output) its
+// solutions, statuses and iteration counts equal the C restatement's bit for bit
+// (tests/test_gpu_wide.py).
+#include "mpcqp_build.h"
+
+namespace {
+using mpcqp::Launch;
+
+constexpr int kT = 256;  // threads per QP
+constexpr int kTW = kT / kWave;
+
+// ---- arena layout (doubles), offsets from the QP's arena base
+struct WideLayout {
+  int N, n, m, ks;  // ks: row stride of K (n + 1: the rows of a column read hit distinct banks)
+  int oK, oModel, oPa, oPg, oE4, oG, oQ, oD, oX, oXt, oRhs, oPx, oAty, oXp, oXa, oDx, oRes, oPd, oXn, oDl, oCol, oCm;
+  int oK1, oK2, oEr, oL, oU, oW, oLo0, oHi0, oW0, oZ, oY, oZt, oTmp, oAx, oRw, oZc, oZn, oZd, oEl, oT1, oT2, oCd, oCn,
+      oRed, total;
+  __host__ __device__ static WideLayout make(int N) {
+    WideLayout L{};
+    L.N = N;
+    L.n = 2 * N;
+    L.m = 5 * N;
+    L.ks = L.n + 1;
+    int o = 0;
+    auto take = [&](int cnt) {
+      const int r = o;
+      o += (cnt + 1) / 2 * 2;  // 16-byte alignment
+      return r;
+    };
+    L.oK = take(L.n * L.ks);
+    L.oModel = take(model_stride(N));
+    L.oPa = take(N + 1);
+    L.oPg = take(N + 1);
+    L.oE4 = take(4 * (N + 1));
+    L.oG = take(L.n + 1);
+    L.oQ = take(L.n);
+    L.oD = take(L.n);
+    L.oX = take(L.n);
+    L.oXt = take(L.n);
+    L.oRhs = take(L.n);
+    L.oPx = take(L.n);
+    L.oAty = take(L.n);
+    L.oXp = take(L.n);
+    L.oXa = take(L.n);
+    L.oDx = take(L.n);
+    L.oRes = take(L.n);
+    L.oPd = take(L.n);
+    L.oXn = take(L.n);
+    L.oDl = take(L.n);
+    L.oCol = take(L.n);
+    L.oCm = take(L.n);
+    L.oK1 = take(2 * L.n);
+    L.oK2 = take(3 * L.n);
+    L.oEr = take(L.m);
+    L.oL = take(L.m);
+    L.oU = take(L.m);
+    L.oW = take(L.m);
+    L.oLo0 = take(L.m);
+    L.oHi0 = take(L.m);
+    L.oW0 = take(L.m);
+    L.oZ = take(L.m);
+    L.oY = take(L.m);
+    L.oZt = take(L.m);
+    L.oTmp = take(L.m);
+    L.oAx = take(L.m);
+    L.oRw = take(L.m);
+    L.oZc = take(L.m);
+    L.oZn = take(L.m);
+    L.oZd = take(L.m);
+    L.oEl = take(L.m);
+    L.oT1 = take(L.m);
+    L.oT2 = take(L.m);
+    L.oCd = take(L.m);  // active codes as doubles (0, 1, 2)
+    L.oCn = take(L.m);
+    L.oRed = take(4 * kTW + 8);
+    L.total = o;
+    return L;
+  }
+};
+
+// per-QP workspace doubles: Pbar (n x n) + the arena (used when it does not fit in LDS)
+__host__ __device__ inline size_t wide_stride_of(const WideLayout& L) { return (size_t)L.n * L.n + L.total; }
+
+// ---- block reductions (maxima: exact, any order; flags)
+struct Blk {
+  double* red;  // 4 * kTW + 8 doubles of the arena
+  __device__ double max(double v) const {  // v >= 0 or NaN-free maxima of |.|
+    for (int o = kWave / 2; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o, kWave));
+    __syncthreads();
+    if ((threadIdx.x & (kWave - 1)) == 0) red[threadIdx.x / kWave] = v;
+    __syncthreads();
+    double r = red[0];
+    for (int k = 1; k < kTW; ++k) r = fmax(r, red[k]);
+    __syncthreads();
+    return r;
+  }
+  __device__ bool any(bool b) const {
+    const bool w = __ballot(b) != 0ull;
+    __syncthreads();
+    if ((threadIdx.x & (kWave - 1)) == 0) red[threadIdx.x / kWave] = w ? 1.0 : 0.0;
+    __syncthreads();
+    bool r = false;
+    for (int k = 0; k < kTW; ++k) r = r || red[k] != 0.0;
+    __syncthreads();
+    return r;
+  }
+  // thread 0's value to every thread
+  __device__ double bcast0(double v) const {
+    __syncthreads();
+    if (threadIdx.x == 0) red[kTW] = v;
+    __syncthreads();
+    const double r = red[kTW];
+    __syncthreads();
+    return r;
+  }
+};
+
+__device__ __forceinline__ double lim(double v) { return limit_scaling(v); }
+
+// The per-QP state of the wide solve: pointers into the arena + the workspace Pbar.
+struct Wide {
+  WideLayout L;
+  double* A;   // arena
+  double* P;   // Pbar, n x n row-major (workspace)
+  Blk blk;
+  int tid;
+  double c;    // cost scaling (uniform)
+  double dt;
+  __device__ double* at(int off) const { return A + off; }
+  __device__ double& K(int i, int j) const { return A[L.oK + i * L.ks + j]; }
+
+  // z = Cbar x (mpcqp_cpu.c Cmul)
+  __device__ void Cmul(const double* x, double* z) const {
+#pragma clang fp contract(off)
+    const int N = L.N, n = L.n;
+    const double* D = at(L.oD);
+    const double* E = at(L.oEr);
+    const double* k1 = at(L.oK1);
+    const double* k2 = at(L.oK2);
+    __syncthreads();
+    for (int j = tid; j < N; j += kT) z[j] = E[j] * (D[2 * j] * x[2 * j]);
+    for (int p = tid; p < n; p += kT) {
+      const double e1 = E[N + p], e2 = E[3 * N + p];
+      const double t0 = D[p] * x[p];
+      const double tm2 = p >= 2 ? D[p - 2] * x[p - 2] : 0.0;
+      const double tm4 = p >= 4 ? D[p - 4] * x[p - 4] : 0.0;
+      z[N + p] = (e1 * k1[2 * p]) * t0 + (e1 * k1[2 * p + 1]) * tm2;
+      z[3 * N + p] = ((e2 * k2[3 * p]) * t0 + (e2 * k2[3 * p + 1]) * tm2) + (e2 * k2[3 * p + 2]) * tm4;
+    }
+    __syncthreads();
+  }
+  // x = Cbar' y (mpcqp_cpu.c CTmul)
+  __device__ void CTmul(const double* y, double* x) const {
+#pragma clang fp contract(off)
+    const int N = L.N, n = L.n;
+    const double* D = at(L.oD);
+    const double* E = at(L.oEr);
+    const double* k1 = at(L.oK1);
+    const double* k2 = at(L.oK2);
+    __syncthreads();
+    for (int p = tid; p < n; p += kT) {
+      const double e1 = E[N + p], e2 = E[3 * N + p];
+      double t = ((p & 1) == 0 ? E[p / 2] * y[p / 2] : 0.0) + (e1 * k1[2 * p]) * y[N + p];
+      t += (e2 * k2[3 * p]) * y[3 * N + p];
+      double a1 = 0.0, b2 = 0.0;  // a1[p + 2], b2[p + 4] of the C code
+      if (p + 2 < n) {
+        const double f1 = E[N + p + 2], f2 = E[3 * N + p + 2];
+        a1 = (f1 * k1[2 * (p + 2) + 1]) * y[N + p + 2] + (f2 * k2[3 * (p + 2) + 1]) * y[3 * N + p + 2];
+      }
+      if (p + 4 < n) b2 = (E[3 * N + p + 4] * k2[3 * (p + 4) + 2]) * y[3 * N + p + 4];
+      t += a1;
+      t += b2;
+      x[p] = D[p] * t;
+    }
+    __syncthreads();
+  }
+  // y = M x, M row-major with row stride ms (thread i: the C code's sequential row sum)
+  __device__ void matvec(const double* M, int ms, const double* x, double* y) const {
+#pragma clang fp contract(off)
+    __syncthreads();
+    for (int i = tid; i < L.n; i += kT) {
+      double t = 0.0;
+      const double* row = M + (size_t)i * ms;
+      for (int j = 0; j < L.n; ++j) t += row[j] * x[j];
+      y[i] = t;
+    }
+    __syncthreads();
+  }
+  // (Pbar + sig I + D (Cbar' diag(rw) Cbar)_band D)[i][j]  (mpcqp_cpu.c form_kkt: the band entry
+  // Bd[i][j] accumulated in the C code's order -- the v row, then rows p = max(i, j), +2, +4,
+  // slot 1 before slot 2 of each)
+  __device__ double kkt(int i, int j, double sig, const double* rw) const {
+#pragma clang fp contract(off)
+    const int N = L.N, n = L.n;
+    const double* D = at(L.oD);
+    const double* E = at(L.oEr);
+    const double* k1 = at(L.oK1);
+    const double* k2 = at(L.oK2);
+    double bd = 0.0;
+    const int dij = i > j ? i - j : j - i;
+    if ((dij & 1) == 0 && dij <= 4) {
+      if (i == j && (i & 1) == 0) bd += E[i / 2] * E[i / 2] * rw[i / 2];
+      const int pm = i > j ? i : j, pl = i > j ? j : i;
+      for (int p = pm; p <= pl + 4 && p < n; p += 2) {
+        const int a = (p - i) / 2, b = (p - j) / 2;  // coefficient a multiplies variable p - 2a = i
+        const double e1 = E[N + p], e2 = E[3 * N + p];
+        if (a < 2 && b < 2) {
+          const double ca = e1 * k1[2 * p + a], cb = e1 * k1[2 * p + b];
+          if (ca != 0.0 && cb != 0.0) bd += rw[N + p] * ca * cb;
+        }
+        const double ca = e2 * k2[3 * p + a], cb = e2 * k2[3 * p + b];
+        if (ca != 0.0 && cb != 0.0) bd += rw[3 * N + p] * ca * cb;
+      }
+    }
+    return P[(size_t)i * n + j] + D[i] * D[j] * bd + (i == j ? sig : 0.0);
+  }
+  __device__ void form(double sig, const double* rw) const {
+    const int n = L.n;
+    __syncthreads();
+    for (int e = tid; e < n * n; e += kT) {
+      const int i = e / n, j = e - (e / n) * n;
+      K(i, j) = kkt(i, j, sig, rw);
+    }
+    __syncthreads();
+  }
+  // y = M x for the Newton matrix M = kkt(., ., 0, rw) (the C code's matvec over its stored M)
+  __device__ void kkt_matvec(const double* rw, const double* x, double* y) const {
+#pragma clang fp contract(off)
+    __syncthreads();
+    for (int i = tid; i < L.n; i += kT) {
+      double t = 0.0;
+      for (int j = 0; j < L.n; ++j) t += kkt(i, j, 0.0, rw) * x[j];
+      y[i] = t;
+    }
+    __syncthreads();
+  }
+  // in-place symmetric sweep K <- K^{-1} (mpcqp_cpu.c sweep_inverse); false on a bad pivot
+  __device__ bool sweep() const {
+#pragma clang fp contract(off)
+    const int n = L.n;
+    double* col = at(L.oCol);
+    for (int k = 0; k < n; ++k) {
+      __syncthreads();
+      const double d = K(k, k);
+      if (!(d > 0.0) || !isfinite(d)) return false;  // uniform: every thread reads the same pivot
+      const double inv = 1.0 / d;
+      for (int i = tid; i < n; i += kT) col[i] = K(i, k);
+      __syncthreads();
+      for (int e = tid; e < n * n; e += kT) {
+        const int i = e / n, j = e - (e / n) * n;
+        if (i == k) {
+          K(k, j) = j == k ? -inv : col[j] * inv;
+        } else if (j == k) {
+          K(i, k) = col[i] * inv;
+        } else {
+          const double f = col[i] * inv;
+          K(i, j) = K(i, j) - f * col[j];
+        }
+      }
+    }
+    __syncthreads();
+    for (int e = tid; e < n * n; e += kT) {
+      const int i = e / n, j = e - (e / n) * n;
+      K(i, j) = -K(i, j);
+    }
+    __syncthreads();
+    return true;
+  }
+  __device__ static int code(double z, double l, double u) { return z > u ? 2 : (z < l ? 1 : 0); }
+};
+
+// condensing + scaling (mpcqp_cpu.c condense + setup_qp); returns bad (non-finite data)
+__device__ bool wide_setup(const mpcqp_params& p, Wide& S) {
+#pragma clang fp contract(off)
+  const WideLayout& L = S.L;
+  const int N = L.N, n = L.n, m = L.m, tid = S.tid;
+  const double* mdl = S.at(L.oModel);
+  const double* al = mdl;
+  const double* be = mdl + N;
+  const double* ga = mdl + 2 * N;
+  const double* et = mdl + 3 * N;
+  const double* si = mdl + 4 * N;
+  const double* c0 = mdl + 5 * N;
+  const double* c1 = mdl + 6 * N;
+  const double* r = mdl + 7 * N;
+  const double* x0 = mdl + 11 * N + 4;
+  const double* up = mdl + 11 * N + 8;
+  const double dt = p.dt;
+  double* Pa = S.at(L.oPa);
+  double* Pg = S.at(L.oPg);
+  double* e4 = S.at(L.oE4);
+  double* g = S.at(L.oG);
+  if (tid == 0) {
+    Pa[0] = Pg[0] = 0.0;
+    for (int k = 0; k < N; ++k) {
+      Pa[k + 1] = Pa[k] + al[k];
+      Pg[k + 1] = Pg[k] + ga[k];
+    }
+  } else if (tid == kWave) {  // free response, another wave
+    double px = x0[0], py = x0[1];
+    const double psi = x0[2];
+    for (int mm = 1; mm <= N; ++mm) {
+      const int k = mm - 1;
+      const double v = k == 0 ? x0[3] : 0.0;
+      px = px + al[k] * psi + be[k] * v + c0[k];
+      py = py + ga[k] * psi + et[k] * v + c1[k];
+      e4[4 * mm + 0] = px - r[4 * mm + 0];
+      e4[4 * mm + 1] = py - r[4 * mm + 1];
+      e4[4 * mm + 2] = psi - r[4 * mm + 2];
+      e4[4 * mm + 3] = 0.0 - r[4 * mm + 3];
+    }
+  }
+  __syncthreads();
+  double Q[4][4], QN[4][4], R[2][2];
+  for (int i = 0; i < 4; ++i)
+    for (int j = 0; j < 4; ++j) {
+      Q[i][j] = 0.5 * (p.q[4 * i + j] + p.q[4 * j + i]);
+      QN[i][j] = 0.5 * (p.q_terminal[4 * i + j] + p.q_terminal[4 * j + i]);
+    }
+  for (int i = 0; i < 2; ++i)
+    for (int j = 0; j < 2; ++j) R[i][j] = 0.5 * (p.r[2 * i + j] + p.r[2 * j + i]);
+  // column `col` of H (the workspace P buffer holds H until P = 2H), col == n -> g
+  for (int col = tid; col <= n; col += kT) {
+    const int j = col >> 1, cc = col & 1;
+    double mu[3] = {0, 0, 0};
+    for (int mm = N; mm >= 1; --mm) {
+      double sv[4];
+      if (col == n) {
+        sv[0] = e4[4 * mm + 0];
+        sv[1] = e4[4 * mm + 1];
+        sv[2] = e4[4 * mm + 2];
+        sv[3] = e4[4 * mm + 3];
+      } else if (cc == 0) {
+        const bool on = mm >= j + 2;
+        sv[0] = on ? be[j + 1] : 0.0;
+        sv[1] = on ? et[j + 1] : 0.0;
+        sv[2] = 0.0;
+        sv[3] = mm == j + 1 ? 1.0 : 0.0;
+      } else if (mm > j) {
+        sv[0] = si[j] * (Pa[mm] - Pa[j + 1]);
+        sv[1] = si[j] * (Pg[mm] - Pg[j + 1]);
+        sv[2] = si[j];
+        sv[3] = 0.0;
+      } else {
+        sv[0] = sv[1] = sv[2] = sv[3] = 0.0;
+      }
+      const bool term = mm == N;
+      double ws[4];
+      for (int a = 0; a < 4; ++a) {
+        const double* W = term ? QN[a] : Q[a];
+        ws[a] = W[0] * sv[0] + W[1] * sv[1] + W[2] * sv[2] + W[3] * sv[3];
+      }
+      double hv;
+      if (mm < N) {
+        const double m0 = mu[0], m1 = mu[1];
+        hv = ws[3] + (be[mm] * m0 + et[mm] * m1);
+        mu[0] = ws[0] + m0;
+        mu[1] = ws[1] + m1;
+        mu[2] = ws[2] + (mu[2] + al[mm] * m0 + ga[mm] * m1);
+      } else {
+        hv = ws[3];
+        mu[0] = ws[0];
+        mu[1] = ws[1];
+        mu[2] = ws[2];
+      }
+      const double hd = si[mm - 1] * mu[2];
+      if (col == n) {
+        g[2 * (mm - 1)] = hv;
+        g[2 * (mm - 1) + 1] = hd;
+      } else {
+        S.P[(size_t)(2 * (mm - 1)) * n + col] = hv;
+        S.P[(size_t)(2 * (mm - 1) + 1) * n + col] = hd;
+      }
+    }
+    const double r00 = R[0][0] / (dt * dt), r10 = R[1][0] / dt;
+    double* H = S.P;
+    if (col == n) {
+      g[0] += -x0[3] * r00;
+      g[1] += -x0[3] * r10;
+    } else if (cc == 0) {
+      H[(size_t)col * n + col] += j + 1 < N ? 2.0 * r00 : r00;
+      if (j >= 1) H[(size_t)(col - 2) * n + col] += -r00;
+      if (j + 1 < N) H[(size_t)(col + 2) * n + col] += -r00;
+      H[(size_t)(col + 1) * n + col] += r10;
+      if (j + 1 < N) H[(size_t)(col + 3) * n + col] += -r10;
+    } else {
+      H[(size_t)(col - 1) * n + col] += r10;
+      if (j >= 1) H[(size_t)(col - 3) * n + col] += -r10;
+      H[(size_t)col * n + col] += R[1][1];
+    }
+  }
+  __syncthreads();
+  double* q = S.at(L.oQ);
+  double* D = S.at(L.oD);
+  double* E = S.at(L.oEr);
+  double* k1 = S.at(L.oK1);
+  double* k2 = S.at(L.oK2);
+  double* lo0 = S.at(L.oLo0);
+  double* hi0 = S.at(L.oHi0);
+  double* w0 = S.at(L.oW0);
+  for (int e = tid; e < n * n; e += kT) S.P[e] = 2.0 * S.P[e];
+  const double idt = 1.0 / p.dt, v0 = x0[3];
+  for (int i = tid; i < n; i += kT) {
+    q[i] = 2.0 * g[i];
+    if ((i & 1) == 0) {
+      k1[2 * i] = idt;
+      k1[2 * i + 1] = i >= 2 ? -idt : 0.0;
+      k2[3 * i] = idt;
+      k2[3 * i + 1] = i >= 2 ? -2.0 * idt : 0.0;
+      k2[3 * i + 2] = i >= 4 ? idt : 0.0;
+    } else {
+      k1[2 * i] = 1.0;
+      k1[2 * i + 1] = 0.0;
+      k2[3 * i] = 1.0;
+      k2[3 * i + 1] = i >= 3 ? -1.0 : 0.0;
+      k2[3 * i + 2] = 0.0;
+    }
+    const int c = i & 1;
+    const double ofa = i == 0 ? v0 * idt : 0.0;
+    const double ofr = i < 2 ? up[c] + ofa : (i == 2 ? -v0 * idt : 0.0);
+    lo0[N + i] = p.u_bounds[2 * c] + ofa;
+    hi0[N + i] = p.u_bounds[2 * c + 1] + ofa;
+    w0[N + i] = p.slack_input;
+    lo0[3 * N + i] = p.du_bounds[2 * c] + ofr;
+    hi0[3 * N + i] = p.du_bounds[2 * c + 1] + ofr;
+    w0[3 * N + i] = p.slack_rate;
+    D[i] = 1.0;
+  }
+  for (int j = tid; j < N; j += kT) {
+    lo0[j] = p.v_bounds[0];
+    hi0[j] = p.v_bounds[1];
+    w0[j] = p.slack_velocity;
+  }
+  for (int rr = tid; rr < m; rr += kT) E[rr] = 1.0;
+  __syncthreads();
+  double* dl = S.at(L.oDl);
+  double* el = S.at(L.oEl);
+  double* cm = S.at(L.oCm);
+  double c = 1.0, cpend = 1.0;
+  for (int it = 0; it < p.scaling; ++it) {
+    for (int qq = tid; qq < n; qq += kT) {
+      double cp = 0.0;
+      for (int i = 0; i < n; ++i) cp = fmax(cp, fabs(S.P[(size_t)i * n + qq]));
+      cp *= cpend;
+      double cc = (qq & 1) == 0 ? E[qq / 2] : 0.0;
+      cc = fmax(cc, E[N + qq] * fabs(k1[2 * qq]));
+      cc = fmax(cc, E[3 * N + qq] * fabs(k2[3 * qq]));
+      if (qq + 2 < n) {
+        cc = fmax(cc, E[N + qq + 2] * fabs(k1[2 * (qq + 2) + 1]));
+        cc = fmax(cc, E[3 * N + qq + 2] * fabs(k2[3 * (qq + 2) + 1]));
+      }
+      if (qq + 4 < n) cc = fmax(cc, E[3 * N + qq + 4] * fabs(k2[3 * (qq + 4) + 2]));
+      cc *= D[qq];
+      dl[qq] = 1.0 / sqrt(lim(fmax(cp, cc)));
+      const double dm2 = qq >= 2 ? D[qq - 2] : 0.0, dm4 = qq >= 4 ? D[qq - 4] : 0.0;
+      const double r1 = fmax(fabs(k1[2 * qq]) * D[qq], fabs(k1[2 * qq + 1]) * dm2);
+      const double r2 = fmax(fmax(fabs(k2[3 * qq]) * D[qq], fabs(k2[3 * qq + 1]) * dm2), fabs(k2[3 * qq + 2]) * dm4);
+      el[N + qq] = 1.0 / sqrt(lim(E[N + qq] * r1));
+      el[3 * N + qq] = 1.0 / sqrt(lim(E[3 * N + qq] * r2));
+    }
+    for (int j = tid; j < N; j += kT) el[j] = 1.0 / sqrt(lim(E[j] * D[2 * j]));
+    __syncthreads();
+    for (int e = tid; e < n * n; e += kT) {
+      const int i = e / n, j = e - (e / n) * n;
+      const double dlc = dl[j] * cpend;
+      S.P[e] = S.P[e] * (dl[i] * dlc);
+    }
+    for (int i = tid; i < n; i += kT) {
+      D[i] *= dl[i];
+      q[i] *= dl[i];
+    }
+    for (int rr = tid; rr < m; rr += kT) E[rr] *= el[rr];
+    __syncthreads();
+    double qm = 0.0;
+    for (int qq = tid; qq < n; qq += kT) {
+      double cp = 0.0;
+      for (int i = 0; i < n; ++i) cp = fmax(cp, fabs(S.P[(size_t)i * n + qq]));
+      cm[qq] = cp;
+      qm = fmax(qm, fabs(q[qq]));
+    }
+    qm = S.blk.max(qm);  // synchronizes: cm complete
+    double cn = 0.0;
+    for (int qq = 0; qq < n; ++qq) cn += cm[qq];  // every thread, the C code's order
+    cn /= n;
+    const double ct = 1.0 / lim(fmax(cn, lim(qm)));
+    cpend = ct;
+    for (int i = tid; i < n; i += kT) q[i] *= ct;
+    c *= ct;
+    __syncthreads();
+  }
+  for (int e = tid; e < n * n; e += kT) S.P[e] *= cpend;
+  double* l = S.at(L.oL);
+  double* u = S.at(L.oU);
+  double* w = S.at(L.oW);
+  for (int rr = tid; rr < m; rr += kT) {
+    l[rr] = E[rr] * lo0[rr];
+    u[rr] = E[rr] * hi0[rr];
+    w[rr] = c * w0[rr] / (E[rr] * E[rr]);
+  }
+  S.c = c;
+  __syncthreads();
+  bool bad = false;
+  for (int i = tid; i < n; i += kT) bad = bad || !isfinite(q[i]);
+  for (int e = tid; e < n * n; e += kT) bad = bad || !isfinite(S.P[e]);
+  for (int rr = tid; rr < m; rr += kT) bad = bad || !isfinite(l[rr]) || !isfinite(u[rr]);
+  return S.blk.any(bad);
+}
+
+// mpcqp_cpu.c polish_run: 1 exact optimum found (x = it), 0 not within max_it passes, -1 failure
+__device__ int wide_polish(Wide& S, double* x, const double* zg, int max_it, int& pol_it, int& n_fact, int& n_ls) {
+#pragma clang fp contract(off)
+  const WideLayout& L = S.L;
+  const int n = L.n, m = L.m, tid = S.tid;
+  const double* q = S.at(L.oQ);
+  const double* l = S.at(L.oL);
+  const double* u = S.at(L.oU);
+  const double* w = S.at(L.oW);
+  double* cd = S.at(L.oCd);
+  double* cn = S.at(L.oCn);
+  double* zc = S.at(L.oZc);
+  double* rw = S.at(L.oRw);
+  double* tmp = S.at(L.oTmp);
+  double* rhs = S.at(L.oRhs);
+  double* xn = S.at(L.oXn);
+  double* zn = S.at(L.oZn);
+  double* res = S.at(L.oRes);
+  double* dx = S.at(L.oDx);
+  double* Px = S.at(L.oPx);
+  double* Pd = S.at(L.oPd);
+  double* zd = S.at(L.oZd);
+  double* t1 = S.at(L.oT1);
+  double* t2 = S.at(L.oT2);
+  S.Cmul(x, zc);
+  S.matvec(S.P, n, x, Px);
+  for (int r = tid; r < m; r += kT) cd[r] = Wide::code(zg[r], l[r], u[r]);
+  __syncthreads();
+  for (int it = 1; it <= max_it; ++it) {
+    ++pol_it;
+    for (int r = tid; r < m; r += kT) {
+      rw[r] = cd[r] != 0.0 ? 2.0 * w[r] : 0.0;
+      tmp[r] = cd[r] == 2.0 ? rw[r] * u[r] : (cd[r] == 1.0 ? rw[r] * l[r] : 0.0);
+    }
+    S.form(0.0, rw);
+    ++n_fact;
+    if (!S.sweep()) return -1;
+    S.CTmul(tmp, rhs);
+    for (int i = tid; i < n; i += kT) rhs[i] -= q[i];
+    S.matvec(&S.K(0, 0), L.ks, rhs, xn);
+    S.Cmul(xn, zn);
+    bool nf = false, diff = false;
+    for (int i = tid; i < n; i += kT) nf = nf || !isfinite(xn[i]);
+    for (int r = tid; r < m; r += kT) diff = diff || Wide::code(zn[r], l[r], u[r]) != cd[r];
+    if (S.blk.any(nf)) return -1;
+    if (!S.blk.any(diff)) {
+      // the set reproduces itself: one step of iterative refinement, then accept if it still does
+      S.kkt_matvec(rw, xn, res);
+      for (int i = tid; i < n; i += kT) res[i] = rhs[i] - res[i];
+      S.matvec(&S.K(0, 0), L.ks, res, dx);
+      for (int i = tid; i < n; i += kT) xn[i] += dx[i];
+      S.Cmul(xn, zn);
+      nf = false;
+      diff = false;
+      for (int i = tid; i < n; i += kT) nf = nf || !isfinite(xn[i]);
+      for (int r = tid; r < m; r += kT) diff = diff || Wide::code(zn[r], l[r], u[r]) != cd[r];
+      if (S.blk.any(nf)) return -1;
+      if (!S.blk.any(diff)) {
+        for (int i = tid; i < n; i += kT) x[i] = xn[i];
+        __syncthreads();
+        return 1;
+      }
+    }
+    // exact line search along d = xn - x (P xn from the Newton system, no product with P)
+    for (int r = tid; r < m; r += kT)
+      tmp[r] = rw[r] * (zn[r] - (cd[r] == 2.0 ? u[r] : (cd[r] == 1.0 ? l[r] : 0.0)));
+    S.CTmul(tmp, Pd);
+    for (int i = tid; i < n; i += kT) {
+      dx[i] = xn[i] - x[i];
+      Pd[i] = (-Pd[i] - q[i]) - Px[i];
+    }
+    for (int r = tid; r < m; r += kT) zd[r] = zn[r] - zc[r];
+    __syncthreads();
+    double qd = 0.0, lin = 0.0;  // every thread, the C code's order
+    for (int i = 0; i < n; ++i) {
+      qd += dx[i] * Pd[i];
+      lin += (Px[i] + q[i]) * dx[i];
+    }
+    double t = 1.0;
+    for (int ls = 0; ls < 40; ++ls) {
+      ++n_ls;
+      for (int r = tid; r < m; r += kT) {
+        const double zt = zc[r] + t * zd[r];
+        const double rr = zt > u[r] ? zt - u[r] : (zt < l[r] ? zt - l[r] : 0.0);
+        t1[r] = 2.0 * w[r] * rr * zd[r];
+        t2[r] = rr != 0.0 ? 2.0 * w[r] * zd[r] * zd[r] : -1.0;  // -1: not added (the term is >= 0)
+      }
+      __syncthreads();
+      double d1 = lin + t * qd, d2 = qd;
+      for (int r = 0; r < m; ++r) {  // the C code's order; d2 takes the rows with rr != 0 only
+        d1 += t1[r];
+        if (t2[r] >= 0.0) d2 += t2[r];
+      }
+      __syncthreads();
+      if (d1 <= 0.0 || !(d2 > 0.0)) break;
+      const double tn = fmax(0.0, t - d1 / d2);
+      if (tn >= t) break;
+      bool moved = false;
+      for (int r = tid; r < m; r += kT) {
+        const double za = zc[r] + t * zd[r], zb = zc[r] + tn * zd[r];
+        moved = moved || Wide::code(za, l[r], u[r]) != Wide::code(zb, l[r], u[r]);
+      }
+      t = tn;
+      if (!S.blk.any(moved)) break;
+    }
+    for (int i = tid; i < n; i += kT) {
+      x[i] += t * dx[i];
+      Px[i] += t * Pd[i];
+    }
+    S.Cmul(x, zc);
+    for (int r = tid; r < m; r += kT) cd[r] = Wide::code(zc[r], l[r], u[r]);
+    __syncthreads();
+  }
+  return 0;
+}
+
+// mpcqp_cpu.c mpcqp_cpu_solve_one after setup: ADMM (+ early polish), final polish, outputs
+__device__ void wide_solve(const mpcqp_params& p, Wide& S, bool bad, int b, double* __restrict__ u0o,
+                           double* __restrict__ Xo, double* __restrict__ Uo, int32_t* __restrict__ statuso,
+                           int32_t* __restrict__ iterso, uint8_t* __restrict__ activeo) {
+#pragma clang fp contract(off)
+  const WideLayout& L = S.L;
+  const int N = L.N, n = L.n, m = L.m, tid = S.tid;
+  const double* q = S.at(L.oQ);
+  const double* D = S.at(L.oD);
+  const double* E = S.at(L.oEr);
+  const double* l = S.at(L.oL);
+  const double* u = S.at(L.oU);
+  const double* w = S.at(L.oW);
+  double* x = S.at(L.oX);
+  double* xt = S.at(L.oXt);
+  double* rhs = S.at(L.oRhs);
+  double* z = S.at(L.oZ);
+  double* y = S.at(L.oY);
+  double* zt = S.at(L.oZt);
+  double* tmp = S.at(L.oTmp);
+  double* Ax = S.at(L.oAx);
+  double* Px = S.at(L.oPx);
+  double* Aty = S.at(L.oAty);
+  double* xp = S.at(L.oXp);
+  double* xa = S.at(L.oXa);
+  double* rw = S.at(L.oRw);
+  for (int i = tid; i < n; i += kT) x[i] = 0.0;
+  for (int r = tid; r < m; r += kT) z[r] = y[r] = 0.0;
+  __syncthreads();
+  int st = MPCQP_MAX_ITER_REACHED;
+  int admm_it = 0, pol_it = 0, n_fact = 0, n_ls = 0;
+  bool admm_ok = false, polished = false, approx = false;
+  if (p.method == MPCQP_METHOD_ADMM) {
+    double rho = p.rho;
+    const double sig = p.sigma, a = p.alpha;
+    bool refactor = true;
+    for (int it = 1; it <= p.max_iter && !bad; ++it) {
+      if (refactor) {
+        for (int r = tid; r < m; r += kT) rw[r] = rho;
+        S.form(sig, rw);
+        ++n_fact;
+        if (!S.sweep()) {
+          bad = true;
+          break;
+        }
+        refactor = false;
+      }
+      for (int r = tid; r < m; r += kT) tmp[r] = rho * z[r] - y[r];
+      S.CTmul(tmp, rhs);
+      for (int i = tid; i < n; i += kT) rhs[i] += sig * x[i] - q[i];
+      S.matvec(&S.K(0, 0), L.ks, rhs, xt);
+      S.Cmul(xt, zt);
+      for (int i = tid; i < n; i += kT) x[i] = a * xt[i] + (1.0 - a) * x[i];
+      const double ir = 1.0 / rho;
+      for (int r = tid; r < m; r += kT) {
+        const double v = a * zt[r] + (1.0 - a) * z[r];
+        const double vv = v + y[r] * ir;
+        double zn = vv;
+        if (vv > u[r])
+          zn = (rho * vv + 2.0 * w[r] * u[r]) / (rho + 2.0 * w[r]);
+        else if (vv < l[r])
+          zn = (rho * vv + 2.0 * w[r] * l[r]) / (rho + 2.0 * w[r]);
+        y[r] = y[r] + rho * (v - zn);
+        z[r] = zn;
+      }
+      __syncthreads();
+      admm_it = it;
+      if (it % p.check_termination == 0 || it == p.max_iter) {
+        S.Cmul(x, Ax);
+        S.matvec(S.P, n, x, Px);
+        S.CTmul(y, Aty);
+        double pr = 0, nAx = 0, nz = 0, spr = 0, snAx = 0, snz = 0;
+        double du = 0, nPx = 0, nAty = 0, nq = 0, sdu = 0, snPx = 0, snAty = 0, snq = 0;
+        for (int r = tid; r < m; r += kT) {
+          const double ie = 1.0 / E[r];
+          pr = fmax(pr, fabs((Ax[r] - z[r]) * ie));
+          nAx = fmax(nAx, fabs(Ax[r] * ie));
+          nz = fmax(nz, fabs(z[r] * ie));
+          spr = fmax(spr, fabs(Ax[r] - z[r]));
+          snAx = fmax(snAx, fabs(Ax[r]));
+          snz = fmax(snz, fabs(z[r]));
+        }
+        for (int i = tid; i < n; i += kT) {
+          const double id = 1.0 / D[i];
+          const double rd = Px[i] + q[i] + Aty[i];
+          du = fmax(du, fabs(rd * id));
+          nPx = fmax(nPx, fabs(Px[i] * id));
+          nAty = fmax(nAty, fabs(Aty[i] * id));
+          nq = fmax(nq, fabs(q[i] * id));
+          sdu = fmax(sdu, fabs(rd));
+          snPx = fmax(snPx, fabs(Px[i]));
+          snAty = fmax(snAty, fabs(Aty[i]));
+          snq = fmax(snq, fabs(q[i]));
+        }
+        bool nonfinite = false;  // fmax drops NaNs: test the iterate itself
+        for (int i = tid; i < n; i += kT) nonfinite = nonfinite || !isfinite(x[i]);
+        for (int r = tid; r < m; r += kT) nonfinite = nonfinite || !isfinite(z[r]) || !isfinite(y[r]);
+        pr = S.blk.max(pr);
+        nAx = S.blk.max(nAx);
+        nz = S.blk.max(nz);
+        spr = S.blk.max(spr);
+        snAx = S.blk.max(snAx);
+        snz = S.blk.max(snz);
+        du = S.blk.max(du);
+        nPx = S.blk.max(nPx);
+        nAty = S.blk.max(nAty);
+        nq = S.blk.max(nq);
+        sdu = S.blk.max(sdu);
+        snPx = S.blk.max(snPx);
+        snAty = S.blk.max(snAty);
+        snq = S.blk.max(snq);
+        nonfinite = S.blk.any(nonfinite);
+        const double ic = 1.0 / S.c;
+        du *= ic;
+        const double ep = p.eps_abs + p.eps_rel * fmax(nAx, nz);
+        const double ed = p.eps_abs + p.eps_rel * fmax(fmax(nPx, nAty), nq) * ic;
+        if (nonfinite || !isfinite(pr) || !isfinite(du)) {
+          bad = true;
+          break;
+        }
+        if (pr <= ep && du <= ed) {
+          admm_ok = true;
+          break;
+        }
+        if (it == p.max_iter) {
+          approx = pr <= 10.0 * p.eps_abs + 10.0 * p.eps_rel * fmax(nAx, nz) &&
+                   du <= 10.0 * p.eps_abs + 10.0 * p.eps_rel * fmax(fmax(nPx, nAty), nq) * ic;
+          break;
+        }
+        const bool near = p.polish_near > 0.0 && it >= 2 * p.check_termination &&
+                          fmax(pr / ep, du / ed) < p.polish_near;
+        if (p.polish && p.polish_from > 0 && (it >= p.polish_from || near) && it < p.max_iter) {
+          for (int i = tid; i < n; i += kT) xp[i] = x[i];
+          __syncthreads();
+          const int pr_ = wide_polish(S, xp, z, p.polish_attempt_max_iter, pol_it, n_fact, n_ls);
+          if (pr_ < 0) {
+            bad = true;
+            break;
+          }
+          if (pr_ > 0) {
+            for (int i = tid; i < n; i += kT) x[i] = xp[i];
+            __syncthreads();
+            polished = true;
+            break;
+          }
+          refactor = true;
+        }
+        if (p.adaptive_rho && it % p.adaptive_rho_interval == 0) {
+          const double pn = spr / (fmax(snAx, snz) + kDivTol);
+          const double dn = sdu / (fmax(fmax(snPx, snAty), snq) + kDivTol);
+          double rn = rho * sqrt(pn / (dn + kDivTol));
+          rn = fmin(fmax(rn, kRhoMin), kRhoMax);
+          if (rn > rho * p.adaptive_rho_tolerance || rn < rho / p.adaptive_rho_tolerance) {
+            rho = rn;
+            refactor = true;
+          }
+        }
+      }
+    }
+    st = admm_ok ? MPCQP_SOLVED : (approx ? MPCQP_SOLVED_INACCURATE : MPCQP_MAX_ITER_REACHED);
+  }
+  const bool do_polish = p.method == MPCQP_METHOD_NEWTON ? true : (p.polish != 0 && admm_ok);
+  for (int i = tid; i < n; i += kT) xa[i] = x[i];
+  __syncthreads();
+  if (polished) {
+    st = MPCQP_SOLVED;
+  } else if (do_polish && !bad) {
+    double* zc = S.at(L.oZc);
+    const double* zg = z;
+    if (p.method != MPCQP_METHOD_ADMM) {
+      S.Cmul(x, zt);  // the C code's zc: C x at the start (x = 0)
+      zg = zt;
+    }
+    (void)zc;
+    const int r_ = wide_polish(S, x, zg, p.polish_max_iter, pol_it, n_fact, n_ls);
+    if (r_ < 0) {
+      bad = true;
+    } else if (r_ > 0) {
+      st = MPCQP_SOLVED;
+    } else if (p.method == MPCQP_METHOD_ADMM) {
+      for (int i = tid; i < n; i += kT) x[i] = xa[i];
+      __syncthreads();
+      st = admm_ok ? MPCQP_SOLVED_INACCURATE : MPCQP_MAX_ITER_REACHED;
+    } else {
+      st = MPCQP_MAX_ITER_REACHED;
+    }
+  }
+  bool nf = false;
+  for (int i = tid; i < n; i += kT) nf = nf || !isfinite(x[i]);
+  if (S.blk.any(nf)) bad = true;
+  if (bad) st = MPCQP_NUMERICAL_ERROR;
+
+  // ---- outputs (unscaled): speeds W -> accelerations, states by the LTV recursion
+  const double* mdl = S.at(L.oModel);
+  const double* al = mdl;
+  const double* be = mdl + N;
+  const double* ga = mdl + 2 * N;
+  const double* et = mdl + 3 * N;
+  const double* si = mdl + 4 * N;
+  const double* c0 = mdl + 5 * N;
+  const double* c1 = mdl + 6 * N;
+  const double* x0 = mdl + 11 * N + 4;
+  const double* up = mdl + 11 * N + 8;
+  double* Wv = S.at(L.oXt);  // reuse: W
+  double* Uv = S.at(L.oRhs);  // reuse: U (interleaved a, delta)
+  for (int i = tid; i < n; i += kT) Wv[i] = D[i] * x[i];
+  __syncthreads();
+  for (int k = tid; k < N; k += kT) {
+    Uv[2 * k] = (Wv[2 * k] - (k == 0 ? x0[3] : Wv[2 * k - 2])) / p.dt;
+    Uv[2 * k + 1] = Wv[2 * k + 1];
+  }
+  __syncthreads();
+  double* Xb = Xo ? Xo + (size_t)b * 4 * (N + 1) : nullptr;
+  if (tid == 0) {
+    double X0 = x0[0], X1 = x0[1], X2 = x0[2], X3 = x0[3];
+    for (int k = 0; k <= N; ++k) {
+      if (Xb) {
+        Xb[0 * (N + 1) + k] = X0;
+        Xb[1 * (N + 1) + k] = X1;
+        Xb[2 * (N + 1) + k] = X2;
+        Xb[3 * (N + 1) + k] = X3;
+      }
+      if (activeo) activeo[(size_t)b * (5 * N + 1) + k] = X3 > p.v_bounds[1] ? 2 : (X3 < p.v_bounds[0] ? 1 : 0);
+      if (k == N) break;
+      const double psi = X2, v = X3;
+      const double nx0 = X0 + al[k] * psi + be[k] * v + c0[k];
+      const double nx1 = X1 + ga[k] * psi + et[k] * v + c1[k];
+      X2 = psi + si[k] * Uv[2 * k + 1];
+      X3 = Wv[2 * k];
+      X0 = nx0;
+      X1 = nx1;
+    }
+    statuso[b] = st;
+    if (iterso) {
+      iterso[4 * (size_t)b + 0] = admm_it;
+      iterso[4 * (size_t)b + 1] = pol_it;
+      iterso[4 * (size_t)b + 2] = n_fact;
+      iterso[4 * (size_t)b + 3] = n_ls;
+    }
+    if (u0o) {
+      u0o[2 * (size_t)b] = Uv[0];
+      u0o[2 * (size_t)b + 1] = Uv[1];
+    }
+  }
+  for (int qq = tid; qq < n; qq += kT) {
+    const int c = qq & 1, k = qq >> 1;
+    if (Uo) Uo[(size_t)b * n + c * N + k] = Uv[qq];
+    if (activeo) {
+      uint8_t* ab = activeo + (size_t)b * (5 * N + 1);
+      const double uu = Uv[qq];
+      ab[N + 1 + qq] = uu > p.u_bounds[2 * c + 1] ? 2 : (uu < p.u_bounds[2 * c] ? 1 : 0);
+      const double d = uu - (qq < 2 ? up[c] : Uv[qq - 2]);
+      ab[3 * N + 1 + qq] = d > p.du_bounds[2 * c + 1] ? 2 : (d < p.du_bounds[2 * c] ? 1 : 0);
+    }
+  }
+}
+
+__global__ __launch_bounds__(kT) void k_solve_wide(mpcqp_params p, int B, const uint8_t* __restrict__ mask,
+                                                   const double* __restrict__ model, double* __restrict__ wide,
+                                                   int arena_lds, double* __restrict__ u0o, double* __restrict__ Xo,
+                                                   double* __restrict__ Uo, int32_t* __restrict__ statuso,
+                                                   int32_t* __restrict__ iterso, uint8_t* __restrict__ activeo) {
+  extern __shared__ double lds[];
+  const int b = blockIdx.x;
+  if (b >= B || (mask && !mask[b])) return;
+  const int N = p.horizon, n = 2 * N;
+  Wide S;
+  S.L = WideLayout::make(N);
+  S.tid = threadIdx.x;
+  S.dt = p.dt;
+  S.c = 1.0;
+  double* qp = wide + (size_t)b * wide_stride_of(S.L);
+  S.P = qp;
+  S.A = arena_lds ? lds : qp + (size_t)n * n;
+  S.blk.red = S.A + S.L.oRed;
+  const double* mb = model + (size_t)b * model_stride(N);
+  for (int i = S.tid; i < model_stride(N); i += kT) S.A[S.L.oModel + i] = mb[i];
+  __syncthreads();
+  const bool bad = wide_setup(p, S);
+  wide_solve(p, S, bad, b, u0o, Xo, Uo, statuso, iterso, activeo);
+}
+
+}  // namespace
+
+namespace mpcqp {
+size_t wide_stride(int horizon) { return wide_stride_of(WideLayout::make(horizon)); }
+
+// LDS bytes of the arena when it is placed on chip, 0 when it goes to the workspace
+static size_t wide_lds_bytes(int horizon) {
+  const size_t bytes = sizeof(double) * (size_t)WideLayout::make(horizon).total;
+  return bytes <= 160u * 1024u ? bytes : 0;
+}
+
+void launch_solve_wide(hipStream_t s, const Launch& L) {
+  double* wide = L.state;
+  const size_t lds = wide_lds_bytes(L.p->horizon);
+  if (lds > 65536) (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_solve_wide),
+                                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  hipLaunchKernelGGL(k_solve_wide, dim3(L.B), dim3(kT), lds, s, *L.p, L.B, L.mask, L.model, wide, lds > 0 ? 1 : 0,
+                     L.u0, L.X, L.U, L.st, L.it, L.ac);
+}
+}  // namespace mpcqp

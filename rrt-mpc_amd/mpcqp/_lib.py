@@ -17,7 +17,8 @@ LIB_NAME = "libmpcqp.so"
 LIB_PATH = Path(os.environ.get("MPCQP_LIB", Path(__file__).resolve().parent / LIB_NAME))
 
 # constants mirrored from include/mpcqp.h
-MAX_HORIZON = 31
+MAX_HORIZON = 63
+WIDE_MIN_HORIZON = 32  # MPCQP_WIDE_MIN_HORIZON: one 256-thread workgroup per QP from here on
 SOLVED = 1
 SOLVED_INACCURATE = 2
 MAX_ITER_REACHED = -2
@@ -33,7 +34,7 @@ STATUS_NAMES = {
 
 # OSQP settings used by the reference (src/control/mpc_controller.py:121-131) plus the
 # OSQP defaults it relies on implicitly.
-ABI_VERSION = 3  # MPCQP_ABI_VERSION (include/mpcqp.h)
+ABI_VERSION = 4  # MPCQP_ABI_VERSION (include/mpcqp.h)
 
 DEFAULT_SOLVER_SETTINGS = dict(
     rho=0.1,

@@ -56,7 +56,7 @@ def _check_against_oracle(params, x0, ref, u_prev, out, idx):
 def test_batches_match_exact_oracle(cuda, cfg):
     from mpcqp import scenarios
 
-    batch = {"config2": lambda: scenarios.config2(256), "config3": lambda: scenarios.config3(512),
+    batch = {"config2": lambda: scenarios.config2(1024), "config3": lambda: scenarios.config3(512),
              "config4": lambda: scenarios.config4(512)}[cfg]()
     params = _params(batch.horizon)
     out = _solve(params, batch.x0, batch.ref, batch.u_prev)
@@ -132,6 +132,37 @@ def test_k1_model_matches_restatement(cuda):
     ctrl.close()
 
 
+def test_k1_unwrap_golden_exact_pi(cuda, golden):
+    """The reference-generated np.unwrap fixtures (unwrap.npz: exact +-pi jumps, whose sign rule
+    is numpy's `ddmod == -pi and dd > 0`) through K1 on the GPU, bit for bit."""
+    import ctypes
+
+    import torch
+    from mpcqp import _lib
+    from mpcqp.control.mpc_controller import BatchedMPCController
+
+    g = golden("unwrap.npz")
+    hip = ctypes.CDLL("libamdhip64.so")
+    hip.hipMemcpy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
+    for case in range(len(g["lens"])):
+        n = int(g["lens"][case])
+        N = n - 1
+        ref = np.zeros((2, n, 4))
+        ref[:, :, 0] = np.arange(n)
+        ref[:, :, 2] = g["p"][case, :n]
+        ref[:, :, 3] = 10.0
+        ctrl = BatchedMPCController(_params(N), 2, device="cuda:0")
+        ctrl.solve_batch(np.zeros((2, 4)), ref, np.zeros((2, 2)))
+        torch.cuda.synchronize()
+        S = _lib.lib().mpcqp_model_stride(N)
+        host = np.zeros((2, S))
+        assert hip.hipMemcpy(host.ctypes.data, _lib.lib().mpcqp_model_buffer(ctrl._ws), host.nbytes, 2) == 0
+        yaw = host[:, 7 * N + 2: 11 * N + 4: 4]
+        assert np.array_equal(yaw[0], g["unwrapped"][case, :n]), case
+        assert np.array_equal(yaw[1], g["unwrapped"][case, :n]), case
+        ctrl.close()
+
+
 @pytest.mark.parametrize("N", [1, 2, 5, 10, 15, 31])
 def test_horizons(cuda, N):
     from mpcqp import scenarios
@@ -197,7 +228,7 @@ def test_empty_batch_and_errors(cuda):
     assert L.mpcqp_build(ctrl._ws, 5, x0.data_ptr(), ref.data_ptr(), None, None) == -3  # > max_batch
     assert L.mpcqp_solve(ctrl._ws, 3, None, None, None, st.data_ptr(), None, None, None) == -5  # B != built
     bad = _lib.to_c_params(params)
-    bad.horizon = 40
+    bad.horizon = 64  # past MPCQP_MAX_HORIZON
     ws = ctypes.c_void_p()
     assert L.mpcqp_create(ctypes.byref(bad), 4, 0, ctypes.byref(ws)) == -2
     assert b"horizon" in L.mpcqp_last_error()

@@ -1,0 +1,145 @@
+"""Long horizons (N >= 32): the workgroup-per-QP kernel (csrc/mpcqp_wide.hip).
+
+The reference builds its QP for any horizon (src/control/mpc_controller.py:47-57).  Horizons
+32..63 run one 256-thread workgroup per QP (the arena in LDS up to N ~ 48, in the workspace
+beyond).  Checks:
+  * the exact oracle (mpc_oracle.solve_exact): U / X / u0 to 1e-8 relative, identical active sets;
+  * the C restatement fed the GPU's own LTV model (K1 output): U, X, statuses AND iteration
+    counts identical bit for bit -- the kernel is the C code parallelised without changing a
+    floating-point operation;
+  * the drop-in surface: MPCController(MPCConfig(horizon=40)) and a fleet at N = 40.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+REL_TOL = 1e-8
+
+
+def _params(N):
+    from mpcqp.config import MPCConfig
+
+    return MPCConfig(horizon=N).to_parameters(0.8)
+
+
+def _rel(a, b):
+    return float(np.abs(a - b).max() / max(1.0, np.abs(b).max()))
+
+
+def _solve_with_model(params, x0, ref, u_prev, **settings):
+    import torch
+    from mpcqp import _lib
+    from mpcqp.control.mpc_controller import BatchedMPCController
+
+    N = int(params.horizon)
+    B = len(x0)
+    ctrl = BatchedMPCController(params, B, device="cuda:0", **settings)
+    sol = ctrl.solve_batch(x0, ref, u_prev)
+    torch.cuda.synchronize()
+    out = {k: getattr(sol, k).cpu().numpy().copy() for k in sol._fields}
+    L = _lib.lib()
+    model = np.zeros((B, L.mpcqp_model_stride(N)))
+    hip = ctypes.CDLL("libamdhip64.so")
+    hip.hipMemcpy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
+    assert hip.hipMemcpy(model.ctypes.data, L.mpcqp_model_buffer(ctrl._ws), model.nbytes, 2) == 0
+    ctrl.close()
+    return out, model
+
+
+@pytest.mark.parametrize("N", [32, 40, 48, 63])
+def test_long_horizons_match_exact_oracle(cuda, N):
+    import mpc_oracle as mo
+    from mpcqp import scenarios
+
+    batch = scenarios.config3(24, horizon=N, seed=300 + N)
+    params = _params(N)
+    out, _ = _solve_with_model(params, batch.x0, batch.ref, batch.u_prev)
+    assert (out["status"] == 1).all(), np.unique(out["status"], return_counts=True)
+    for b in range(batch.size):
+        ex = mo.solve_exact(params, batch.x0[b], batch.ref[b], batch.u_prev[b])
+        assert ex.converged
+        e = max(_rel(out["U"][b], ex.Umat), _rel(out["X"][b], ex.X), _rel(out["u0"][b], ex.Umat[:, 0]))
+        assert e <= REL_TOL, f"N={N} QP {b}: rel err {e:.3e}"
+        assert np.array_equal(out["active"][b], ex.active), f"N={N} QP {b}: active set differs"
+
+
+@pytest.mark.parametrize("N,settings", [(32, {}), (40, {}), (40, {"polish_near": 0.0}),
+                                        (48, {"polish_from": 0, "polish_near": 0.0}), (63, {})])
+def test_long_horizons_bit_exact_with_c_restatement(cuda, N, settings):
+    """Same model in -> same bits out: solutions, statuses, ADMM/polish/factorization/line-search
+    counts all identical to oracle/mpcqp_cpu.c (100 % of QPs, not a majority)."""
+    import cpu_solver
+    from mpcqp import scenarios
+
+    batch = scenarios.config3(48, horizon=N, seed=700 + N)
+    params = _params(N)
+    out, model = _solve_with_model(params, batch.x0, batch.ref, batch.u_prev, **settings)
+    ref = cpu_solver.cpu_solve_models(params, model, **settings)
+    assert np.array_equal(out["status"], ref["status"])
+    assert np.array_equal(out["iters"], ref["iters"]), np.argwhere((out["iters"] != ref["iters"]).any(axis=1))
+    assert np.array_equal(out["U"], ref["U"])
+    assert np.array_equal(out["X"], ref["X"])
+    assert np.array_equal(out["active"], ref["active"])
+
+
+def test_long_horizon_newton_and_max_iter(cuda):
+    """Method newton and an ADMM capped below convergence: statuses and counts as the C code."""
+    import cpu_solver
+    from mpcqp import scenarios
+
+    N = 36
+    batch = scenarios.config3(32, horizon=N, seed=9)
+    params = _params(N)
+    for method, settings in (("newton", {}), ("admm", dict(max_iter=40, polish_from=0, polish_near=0.0))):
+        out, model = _solve_with_model(params, batch.x0, batch.ref, batch.u_prev, method=method, **settings)
+        ref = cpu_solver.cpu_solve_models(params, model, method=1 if method == "newton" else 0, **settings)
+        assert np.array_equal(out["status"], ref["status"]), method
+        assert np.array_equal(out["iters"], ref["iters"]), method
+        assert np.array_equal(out["U"], ref["U"]), method
+
+
+def test_mpc_controller_drop_in_at_horizon_40(cuda):
+    """MPCController(params).solve at a horizon the one-wave kernel cannot hold, with a window
+    longer than N+1 rows (the reference reads rows 0..N)."""
+    import mpc_oracle as mo
+    from mpcqp.config import MPCConfig
+    from mpcqp.control.mpc_controller import MPCController
+    from mpcqp import scenarios
+    from mpcqp.control.ref_builder import build_reference
+
+    plan = scenarios.load_default_plan()
+    ref_g = build_reference(plan["path"], 15.0, 40, 0.1)
+    params = MPCConfig(horizon=40).to_parameters(0.8)
+    x0 = np.array([plan["start"][0], plan["start"][1], float(plan["yaw0"]), 5.0])
+    u0, X, U = MPCController(params).solve(x0, ref_g[:45], u_prev=np.zeros(2))
+    ex = mo.solve_exact(params, x0, ref_g[:41], np.zeros(2))
+    assert _rel(U, ex.Umat) <= REL_TOL and _rel(X, ex.X) <= REL_TOL
+    assert X.shape == (4, 41) and U.shape == (2, 40)
+
+
+def test_fleet_at_horizon_40(cuda):
+    """The device closed loop at N = 40 (k_fleet_build + the long-horizon solve) against the
+    oracle's restatement of control_stage.py:84-150 on the same plans."""
+    import mpc_oracle as mo
+    from mpcqp import scenarios
+    from mpcqp.config import MPCConfig
+    from mpcqp.pipeline.fleet import FleetTracker, initial_state
+
+    N, V, steps = 40, 4, 30
+    paths, starts, goals = scenarios.fleet5(V, seed=21)
+    mpc = MPCConfig(horizon=N, sim_steps=steps)
+    ft = FleetTracker(mpc, map_resolution=0.8, max_vehicles=V, max_ref_len=200, device="cuda:0")
+    refs = ft.reset_from_plans(paths, starts, goals)
+    res = ft.run()
+    params = mpc.to_parameters(0.8)
+    for v in range(V):
+        s0 = initial_state(paths[v], starts[v])
+        states = mo.track_loop(params, refs[v], s0[:2], s0[2], goals[v], steps)
+        assert len(states) == len(res.states[v])
+        np.testing.assert_allclose(res.states[v], np.asarray(states), rtol=0, atol=1e-6)
+    ft.close()

@@ -35,7 +35,7 @@ def test_library_exports_every_header_symbol():
         assert hasattr(handle, name), f"{name} declared in include/mpcqp.h but not exported"
     assert set(decls) == set(_lib_mod.exported_symbols())
     L = _lib_mod.lib()
-    assert L.mpcqp_version() == _lib_mod.ABI_VERSION == 3
+    assert L.mpcqp_version() == _lib_mod.ABI_VERSION == 4
     assert L.mpcqp_num_rows(20) == 101
     assert L.mpcqp_model_stride(20) % 8 == 0
 
@@ -269,4 +269,4 @@ def test_solver_kernel_resources():
     assert sorted(res) == list(range(1, 32))
     for N, r in res.items():
         assert r["Occupancy"] >= 2 and r["AGPRs"] == 0, (N, r)
-        assert r["ScratchSize"] <= (0 if N <= 29 else 64), (N, r)
+        assert r["ScratchSize"] <= (0 if N <= 28 else 64), (N, r)

@@ -70,6 +70,79 @@ def test_condensed_solution_solves_full_formulation(seed):
     assert 0.5 * res.x @ P @ res.x + q @ res.x + r0 >= sol.objective - 1e-9
 
 
+def _pinned_cases():
+    """(N, x0, window, u_prev): windows of the reference's own closed loop (closed_loop.npz) at
+    N = 10 and 15, a config-3 sample at N = 20 and a config-4 sample at N = 30."""
+    from pathlib import Path
+
+    from mpcqp import scenarios
+
+    d = np.load(Path(__file__).resolve().parent / "golden" / "closed_loop.npz")
+    c3 = scenarios.config3(64, horizon=20)
+    c4 = scenarios.config4(64, horizon=30)
+    return [
+        (10, d["N10_x0"][0], d["N10_window"][0], d["N10_u_prev"][0]),
+        (10, d["N10_x0"][30], d["N10_window"][30], d["N10_u_prev"][30]),
+        (15, d["N15_x0"][12], d["N15_window"][12], d["N15_u_prev"][12]),
+        (15, d["N15_x0"][50], d["N15_window"][50], d["N15_u_prev"][50]),
+        (20, c3.x0[5], c3.ref[5], c3.u_prev[5]),
+        (20, c3.x0[41], c3.ref[41], c3.u_prev[41]),
+        (30, c4.x0[3], c4.ref[3], c4.u_prev[3]),
+        (30, c4.x0[17], c4.ref[17], c4.u_prev[17]),
+    ]
+
+
+@pytest.mark.parametrize("case", range(8))
+def test_exact_solution_has_kkt_certificate_on_full_formulation(case):
+    """Independent optimality certificate on the reference's un-condensed QP (11N+5 variables,
+    19N+7 rows of mpc_controller.py:53-117): the lifted exact solution is feasible and there are
+    multipliers with the right signs on its active rows (bounded least squares, scipy) that make
+    the Lagrangian stationary.  A strictly convex QP has exactly one such point."""
+    from scipy.optimize import lsq_linear
+
+    N, x0, ref, up = _pinned_cases()[case]
+    p = mo.default_params(N)
+    sol = mo.solve_exact(p, x0, ref, up)
+    assert sol.converged
+    P, q, r0, A, lo, hi, lay = mo.full_qp(p, x0, ref, up)
+    xs = mo.lift(p, sol, up)
+    z = A @ xs
+    tol = 1e-9 * np.maximum(1.0, np.abs(z))
+    assert np.all(z >= lo - tol) and np.all(z <= hi + tol)
+    eq = lo == hi
+    at_hi = ~eq & np.isfinite(hi) & (np.abs(z - hi) <= tol)
+    at_lo = ~eq & np.isfinite(lo) & (np.abs(z - lo) <= tol)
+    act = eq | at_hi | at_lo
+    # L = f + y'(Ax): y >= 0 on rows at their upper bound, y <= 0 at the lower bound
+    lb = np.where(at_hi[act], 0.0, -np.inf)
+    ub = np.where(at_lo[act], 0.0, np.inf)
+    g = P @ xs + q
+    fit = lsq_linear(A[act].T, -g, bounds=(lb, ub), lsmr_tol="auto", method="bvls")
+    stat = np.abs(A[act].T @ fit.x + g).max()
+    assert stat <= 1e-8 * max(1.0, np.abs(g).max()), f"N={N}: stationarity residual {stat:.3e}"
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("case", [0, 2, 4, 6])
+def test_exact_solution_matches_trust_constr(case):
+    """scipy trust-constr (an interior-point solver, nothing shared with the oracle) on the
+    un-condensed formulation at N = 10, 15, 20, 30 agrees with the exact solve's inputs to 1e-6
+    and cannot beat its objective (SURVEY.md §8c3 ii)."""
+    from scipy.optimize import LinearConstraint, minimize
+
+    N, x0, ref, up = _pinned_cases()[case]
+    p = mo.default_params(N)
+    sol = mo.solve_exact(p, x0, ref, up)
+    P, q, r0, A, lo, hi, lay = mo.full_qp(p, x0, ref, up)
+    xs = mo.lift(p, sol, up)
+    res = minimize(lambda v: 0.5 * v @ P @ v + q @ v, np.zeros_like(xs), jac=lambda v: P @ v + q,
+                   hess=lambda v: P, method="trust-constr", constraints=[LinearConstraint(A, lo, hi)],
+                   options=dict(gtol=1e-12, xtol=1e-14, maxiter=6000))
+    dU = np.abs(res.x[lay["oU"]: lay["oSv"]] - xs[lay["oU"]: lay["oSv"]]).max()
+    assert dU <= 1e-6 * max(1.0, np.abs(xs[lay["oU"]: lay["oSv"]]).max()), f"N={N}: |dU| {dU:.3e}"
+    assert 0.5 * res.x @ P @ res.x + q @ res.x + r0 >= sol.objective - 1e-9 * max(1.0, abs(sol.objective))
+
+
 def test_exact_solution_is_stationary():
     rng = np.random.default_rng(5)
     for N in (5, 10, 20):
