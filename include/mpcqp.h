@@ -135,6 +135,9 @@ void mpcqp_destroy(mpcqp_ws* ws);
  *   x0     B x 4
  *   ref    B x (N+1) x 4     [x, y, yaw, v] per row, as ref_traj of solve()
  *   u_prev B x 2             (NULL = zeros, mpc_controller.py:48-49)
+ * For N < MPCQP_WIDE_MIN_HORIZON (and debug_state off) this step is FUSED into the kernel of
+ * the next mpcqp_solve, which reads x0 / ref / u_prev itself: the buffers must stay valid and
+ * unchanged until that solve has run (stream order).  mpcqp_build then enqueues nothing.
  */
 int mpcqp_build(mpcqp_ws* ws, int B, const double* x0, const double* ref, const double* u_prev,
                 void* stream);
@@ -167,6 +170,8 @@ int mpcqp_solve(mpcqp_ws* ws, int B, double* u0, double* X, double* U, int32_t* 
 #define MPCQP_FLEET_GOAL 1        /* hypot(state - goal) < 8 after a step (control_stage.py:147) */
 #define MPCQP_FLEET_ABORTED 2     /* unsolved after relaxation (control_stage.py:108-110) */
 #define MPCQP_FLEET_OUT_OF_STEPS 3 /* steps == max_steps (sim_steps) */
+#define MPCQP_FLEET_REPLAN_RUNNING 4 /* transient inside mpcqp_swarm_step: off track, being replanned */
+#define MPCQP_FLEET_REPLAN_ABORTED 5 /* transient inside mpcqp_swarm_step: aborted, being replanned */
 
 typedef struct mpcqp_fleet {
   int32_t vehicles;          /* V (<= max_batch of both workspaces) */
@@ -266,6 +271,67 @@ int mpcqp_rrt_plan(const mpcqp_rrt_params* p, int V, const uint8_t* occupancy, c
 int mpcqp_rrt_paths(const mpcqp_rrt_params* p, int V, int prune, const uint8_t* occupancy, const double* nodes,
                     const int32_t* count, const int32_t* meta, double* raw, int32_t* raw_len, double* pruned,
                     int32_t* pruned_len, void* stream);
+
+/*
+ * Centripetal Catmull-Rom smoothing (src/planning/rrt_star.py:104-159 with _dedupe_consecutive
+ * :93-101, applied at :264-283) of V paths on the device, one wave each: path v = in[v * in_stride
+ * .. + in_len[v]) points (x, y), out[v * out_stride ..] and out_len[v] points (-1: more than
+ * out_stride points, or more than 4096 after deduplication).  The knot powers |d|^alpha are the
+ * device's (sqrt for alpha = 0.5), within an ulp of the host libm's.
+ */
+int mpcqp_catmull_rom(int V, const double* in, const int32_t* in_len, int in_stride, int samples, double alpha,
+                      double dedupe_tol, double* out, int32_t* out_len, int out_stride, void* stream);
+
+/*
+ * The config-5 swarm: one mpcqp_fleet_step plus, in the same step and on
+ * the device, the replan trigger of the reference's roadmap (README.md:146-148) and the
+ * replanning: a RUNNING vehicle farther than replan_distance from ref_global[path_idx] after its
+ * step, or a vehicle the step ABORTED, with replans left (replans[v] < max_replans), is planned
+ * again from where it stands to its goal -- RRT* (mpcqp_rrt_plan with the PCG64 state
+ * rng_table[v][replans[v]]), path extraction + pruning, Catmull-Rom, build_reference -- and when
+ * that yields a reference it continues on it from path_idx 0 (pose, speed and u_prev carry over);
+ * otherwise it keeps its reference (or stays ABORTED).  Each attempt uses one replan.
+ * The swarm WRITES the fleet's ref_global / ref_len rows of replanned vehicles.
+ * Every pointer is caller-owned device memory; M = rrt.max_iterations + 2, S = fleet ref_stride.
+ */
+typedef struct mpcqp_swarm {
+  mpcqp_rrt_params rrt;      /* planner parameters and grid size */
+  const uint8_t* occupancy;  /* rrt.height x rrt.width, 1 = free (the inflated grid) */
+  int32_t prune;             /* PlannerParameters.prune_path */
+  int32_t spline_samples;    /* PlannerParameters.spline_samples (<= 1: no smoothing) */
+  double spline_alpha;       /* 0.5 */
+  double dedupe_tol;         /* 1e-9 */
+  double desired_speed;      /* build_reference speed (px/s) */
+  double dt;                 /* build_reference dt */
+  int32_t horizon;           /* build_reference horizon (tail padding to horizon + 1 rows) */
+  int32_t max_replans;       /* replans per vehicle (0: the plain fleet step) */
+  double replan_distance;    /* off-track trigger in px (<= 0: only aborted vehicles replan) */
+  int32_t path_cap;          /* smoothed-path capacity per vehicle (points) */
+  int32_t reserved;
+  const uint64_t* rng_table; /* V x max_replans x 4: PCG64 states {state lo, hi, inc lo, hi} */
+  int32_t* replans;          /* V in/out: replans used (set >= max_replans to never replan) */
+  int32_t* replan_step;      /* V x max_replans out (nullable): steps[v] at each replan, -steps-1 if it failed */
+  /* scratch */
+  double* start_goal;        /* V x 4 */
+  double* nodes;             /* V x M x 4 */
+  int32_t* count;            /* V */
+  int32_t* meta;             /* V x 2 */
+  double* raw;               /* V x M x 2 */
+  int32_t* raw_len;          /* V */
+  double* pruned;            /* V x M x 2 */
+  int32_t* pruned_len;       /* V */
+  double* smooth;            /* V x path_cap x 2 */
+  int32_t* smooth_len;       /* V */
+  double* new_ref;           /* V x S x 4 */
+  int32_t* new_len;          /* V */
+} mpcqp_swarm;
+
+/* One closed-loop step of every RUNNING vehicle (mpcqp_fleet_step) + trigger + replanning. */
+int mpcqp_swarm_step(mpcqp_ws* nominal, mpcqp_ws* relaxed, const mpcqp_fleet* f, const mpcqp_swarm* s, void* stream);
+
+/* `steps` swarm steps; use_graph != 0 replays one captured step as a hipGraph (no host round trip). */
+int mpcqp_swarm_run(mpcqp_ws* nominal, mpcqp_ws* relaxed, const mpcqp_fleet* f, const mpcqp_swarm* s, int steps,
+                    int use_graph, void* stream);
 
 /*
  * Occupancy inflation: src/maps/inflate.py:18-51 (the fallback

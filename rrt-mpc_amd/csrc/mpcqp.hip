@@ -138,6 +138,7 @@ int mpcqp_create(const mpcqp_params* p, int max_batch, int device, mpcqp_ws** ws
   w->built_B = -1;
   w->model = nullptr;
   w->state = nullptr;
+  w->in_x0 = w->in_ref = w->in_up = nullptr;
   const size_t mbytes = sizeof(double) * (size_t)model_stride(p->horizon) * (size_t)max_batch;
   const size_t sbytes = sizeof(double) * ws_state_stride(p->horizon) * (size_t)max_batch;
   e = hipMalloc(&w->model, mbytes);
@@ -173,7 +174,16 @@ int mpcqp_build(mpcqp_ws* ws, int B, const double* x0, const double* ref, const 
   if (!ws || !x0 || !ref) return fail(MPCQP_E_ARG, "null argument");
   if (B < 0 || B > ws->max_batch) return fail(MPCQP_E_BATCH, "batch exceeds workspace capacity");
   ws->built_B = B;
+  ws->in_x0 = ws->in_ref = ws->in_up = nullptr;
   if (B == 0) return MPCQP_OK;
+  // The one-wave solve builds the model itself (K1 fused into k_solve: the model block never
+  // touches HBM); the K1 kernel runs only for the long-horizon solve and for inspection builds.
+  if (ws->p.horizon < MPCQP_WIDE_MIN_HORIZON && !ws->p.debug_state) {
+    ws->in_x0 = x0;
+    ws->in_ref = ref;
+    ws->in_up = u_prev;
+    return MPCQP_OK;
+  }
   hipStream_t s = static_cast<hipStream_t>(stream);
   hipLaunchKernelGGL(k_build, dim3(B), dim3(kWave), 0, s, ws->p, B, x0, ref, u_prev, ws->model);
   hipError_t e = hipGetLastError();
@@ -188,6 +198,9 @@ int mpcqp_solve(mpcqp_ws* ws, int B, double* u0, double* X, double* U, int32_t* 
   if (B == 0) return MPCQP_OK;
   hipStream_t s = static_cast<hipStream_t>(stream);
   Launch L{&ws->p, B, ws->model, ws->state, u0, X, U, status, iters, active, nullptr};
+  L.x0 = ws->in_x0;
+  L.ref = ws->in_ref;
+  L.u_prev = ws->in_up;
   mpcqp::launcher(ws->p.horizon)(s, L);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return fail(MPCQP_E_HIP, std::string("k_solve launch: ") + hipGetErrorString(e));

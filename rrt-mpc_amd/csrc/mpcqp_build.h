@@ -6,16 +6,18 @@
 
 namespace {
 
-// One wave per QP, lane k <= N holding window row k = (rx, ry, ryaw, rv):
-//   unwrapped yaw (np.unwrap, mpc_controller.py:59-60), then linearize() at
-//   ref[max(k-1,0)], u = 0 (mpc_controller.py:65-70,108; vehicle_model.py:24-45).
-// x0l = x0[lane] on lanes 0..3, upl = u_prev[lane-4] on lanes 4..5.
-// Model layout per QP (doubles): alpha[N] beta[N] gamma[N] eta[N] sigma[N] c0[N]
-// c1[N] ref[(N+1)*4] x0[4] u_prev[2], stride model_stride(N).
-// Every lane of the wave must call this (DPP reads inactive lanes as zero).
-__device__ __forceinline__ void build_qp(const mpcqp_params& p, int lane, double rx, double ry, double ryaw,
-                                         double rv, double x0l, double upl, double* __restrict__ mb) {
+// The LTV coefficients of lane k < N (step k) and the unwrapped yaw of lane k <= N.
+struct LaneModel {
+  double uyaw, al, be, ga, et, si, c0, c1;
+};
+
+// One wave per QP, lane k <= N holding window row k's yaw and speed: np.unwrap of the yaw
+// (mpc_controller.py:59-60), then linearize() at ref[max(k-1,0)], u = 0 (mpc_controller.py:65-70,
+// 108; vehicle_model.py:24-45).  Every lane of the wave must call this (DPP reads inactive lanes
+// as zero).
+__device__ __forceinline__ LaneModel build_lane(const mpcqp_params& p, int lane, double ryaw, double rv) {
   const int N = p.horizon;
+  LaneModel m{};
   // np.unwrap: ddmod = mod(dd + pi, 2pi) - pi; boundary fix; zero when |dd| < pi
   const double prev = dpp<kWaveShr1>(ryaw);
   double pc = 0.0;
@@ -32,32 +34,49 @@ __device__ __forceinline__ void build_qp(const mpcqp_params& p, int lane, double
     cs = cs + readlane(pc, j);
     if (lane == j) mine = cs;
   }
-  const double uyaw = lane == 0 ? ryaw : ryaw + mine;
-  if (lane <= N) {
-    mb[7 * N + 4 * lane + 0] = rx;
-    mb[7 * N + 4 * lane + 1] = ry;
-    mb[7 * N + 4 * lane + 2] = uyaw;
-    mb[7 * N + 4 * lane + 3] = rv;
-  }
+  m.uyaw = lane == 0 ? ryaw : ryaw + mine;
   // linearisation point of step k: ref[max(k-1, 0)]
-  const double psi_m1 = dpp<kWaveShr1>(uyaw);
+  const double psi_m1 = dpp<kWaveShr1>(m.uyaw);
   const double v_m1 = dpp<kWaveShr1>(rv);
-  const double psi = lane == 0 ? uyaw : psi_m1;
+  const double psi = lane == 0 ? m.uyaw : psi_m1;
   const double v = lane == 0 ? rv : v_m1;
   if (lane < N) {
     const double dt = p.dt, L = p.wheelbase_px;
     const double sec2 = 1.0 / (1.0 * 1.0 + 1e-9);
-    double s, c;
-    sincos(psi, &s, &c);
-    const double al = -dt * v * s;
-    const double ga = dt * v * c;
-    mb[lane] = al;
-    mb[N + lane] = dt * c;
-    mb[2 * N + lane] = ga;
-    mb[3 * N + lane] = dt * s;
-    mb[4 * N + lane] = dt * (v / L) * sec2;
-    mb[5 * N + lane] = -al * psi;
-    mb[6 * N + lane] = -ga * psi;
+    double sn, c;
+    sincos(psi, &sn, &c);
+    m.al = -dt * v * sn;
+    m.be = dt * c;
+    m.ga = dt * v * c;
+    m.et = dt * sn;
+    m.si = dt * (v / L) * sec2;
+    m.c0 = -m.al * psi;
+    m.c1 = -m.ga * psi;
+  }
+  return m;
+}
+
+// build_lane + the model block of one QP written to mb (global or LDS):
+// alpha[N] beta[N] gamma[N] eta[N] sigma[N] c0[N] c1[N] ref[(N+1)*4] x0[4] u_prev[2],
+// stride model_stride(N).  x0l = x0[lane] on lanes 0..3, upl = u_prev[lane-4] on lanes 4..5.
+__device__ __forceinline__ void build_qp(const mpcqp_params& p, int lane, double rx, double ry, double ryaw,
+                                         double rv, double x0l, double upl, double* __restrict__ mb) {
+  const int N = p.horizon;
+  const LaneModel m = build_lane(p, lane, ryaw, rv);
+  if (lane <= N) {
+    mb[7 * N + 4 * lane + 0] = rx;
+    mb[7 * N + 4 * lane + 1] = ry;
+    mb[7 * N + 4 * lane + 2] = m.uyaw;
+    mb[7 * N + 4 * lane + 3] = rv;
+  }
+  if (lane < N) {
+    mb[lane] = m.al;
+    mb[N + lane] = m.be;
+    mb[2 * N + lane] = m.ga;
+    mb[3 * N + lane] = m.et;
+    mb[4 * N + lane] = m.si;
+    mb[5 * N + lane] = m.c0;
+    mb[6 * N + lane] = m.c1;
   }
   if (lane < 6) mb[11 * N + 4 + lane] = lane < 4 ? x0l : upl;
 }

@@ -255,6 +255,11 @@ struct Launch {
   int32_t *st, *it;
   uint8_t* ac;
   const uint8_t* mask;  // QP b is solved iff mask == nullptr or mask[b] != 0 (fleet steps)
+  // K1 fused into the solve: with ref != nullptr the kernel builds each QP's LTV model from the
+  // caller's inputs itself (one-wave kernel); otherwise it reads `model` (K1 / fleet output)
+  const double* x0 = nullptr;
+  const double* ref = nullptr;
+  const double* u_prev = nullptr;
 };
 
 typedef void (*launcher_t)(hipStream_t, const Launch&);
@@ -280,4 +285,8 @@ struct mpcqp_ws {
   int built_B;
   double* model;
   double* state;
+  // the inputs of the last mpcqp_build when the model is built inside the solve (fused K1)
+  const double* in_x0;
+  const double* in_ref;
+  const double* in_up;
 };

@@ -142,6 +142,8 @@ int enqueue_step(mpcqp_ws* nom, mpcqp_ws* rel, const mpcqp_fleet* f, hipStream_t
   if (!solve) return fail(MPCQP_E_HORIZON, "horizon not compiled into this build");
   nom->built_B = -1;  // the fleet overwrites the models: a later mpcqp_solve needs its own build
   rel->built_B = -1;
+  nom->in_x0 = nom->in_ref = nom->in_up = nullptr;
+  rel->in_x0 = rel->in_ref = rel->in_up = nullptr;
   hipLaunchKernelGGL(k_fleet_build, dim3(V), dim3(kWave), 0, s, nom->p, *f, 0, nom->model);
   solve(s, Launch{&nom->p, V, nom->model, nom->state, f->u0, f->X, nullptr, f->status, nullptr, nullptr, f->mask});
   hipLaunchKernelGGL(k_fleet_build, dim3(V), dim3(kWave), 0, s, rel->p, *f, 1, rel->model);

@@ -342,4 +342,97 @@ __device__ void rrt_extract_one(const mpcqp_rrt_params& p, int prune, const uint
   }
 }
 
+// Centripetal Catmull-Rom smoothing of one path on the calling wave (src/planning/rrt_star.py:104-159
+// with _dedupe_consecutive :93-101), numpy's operations in numpy's order, uncontracted:
+//   dedupe: keep a point when ||p - last kept|| > tol (sqrt of dx^2 + dy^2)
+//   n == 1: the point; n == 2: (1 - t) p0 + t p1 on np.linspace(0, 1, max(2, S + 1))
+//   else, segment i of [p0, pts, p_last]: knots t_{j+1} = t_j + (|d|^alpha if |d| > eps else eps),
+//   t on np.linspace(t1, t2, max(2, S + 1), endpoint=False) = k * ((t2 - t1) / num) + t1, then the
+//   Barry-Goldman pyramid; the last point appended.
+// pts: LDS scratch for 2 * cap doubles.  Returns the number of points written (<= out_cap), or
+// -1 when the deduplicated path exceeds cap or the output exceeds out_cap.  |.|^alpha is the
+// device's pow (sqrt for alpha = 0.5), within an ulp of the host libm's.
+__device__ int catmull_rom_one(const double* __restrict__ in, int P, int samples, double alpha, double tol,
+                               double* pts, int cap, double* __restrict__ out, int out_cap) {
+#pragma clang fp contract(off)
+  const int lane = threadIdx.x & (kWave - 1);
+  constexpr double eps = 1e-9;
+  int n = 0;
+  if (lane == 0 && P > 0) {
+    pts[0] = in[0];
+    pts[1] = in[1];
+    n = 1;
+    for (int i = 1; i < P && n >= 0; ++i) {
+      const double dx = in[2 * i] - pts[2 * (n - 1)], dy = in[2 * i + 1] - pts[2 * (n - 1) + 1];
+      if (sqrt(dx * dx + dy * dy) > tol) {
+        if (n == cap) {
+          n = -1;
+          break;
+        }
+        pts[2 * n] = in[2 * i];
+        pts[2 * n + 1] = in[2 * i + 1];
+        ++n;
+      }
+    }
+  }
+  n = __shfl(n, 0, kWave);
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+  __syncthreads();
+  if (n < 0) return -1;
+  if (n <= 1) {
+    if (n == 1 && lane < 2) {
+      if (out_cap < 1) return -1;
+      out[lane] = pts[lane];
+    }
+    return n;
+  }
+  const int num = samples + 1 > 2 ? samples + 1 : 2;
+  if (n == 2) {
+    if (num > out_cap) return -1;
+    const double step = 1.0 / (double)(num - 1);
+    for (int k = lane; k < num; k += kWave) {
+      const double t = k == num - 1 ? 1.0 : (double)k * step + 0.0;
+      out[2 * k] = (1.0 - t) * pts[0] + t * pts[2];
+      out[2 * k + 1] = (1.0 - t) * pts[1] + t * pts[3];
+    }
+    return num;
+  }
+  const int total = (n - 1) * num + 1;
+  if (total > out_cap) return -1;
+  auto knot = [&](double ti, int a, int b) {  // tj(ti, pts[a], pts[b])
+    const double dx = pts[2 * b] - pts[2 * a], dy = pts[2 * b + 1] - pts[2 * a + 1];
+    const double d = sqrt(dx * dx + dy * dy);
+    const double inc = d > eps ? (alpha == 0.5 ? sqrt(d) : pow(d, alpha)) : eps;
+    return ti + inc;
+  };
+  for (int i = 0; i < n - 1; ++i) {
+    // extended points [pts[0], pts..., pts[n-1]]: ext[j] = pts[clamp(j - 1, 0, n - 1)]
+    const int i0 = i - 1 < 0 ? 0 : i - 1, i1 = i, i2 = i + 1, i3 = i + 2 > n - 1 ? n - 1 : i + 2;
+    const double t0 = 0.0;
+    const double t1 = knot(t0, i0, i1);
+    const double t2 = knot(t1, i1, i2);
+    const double t3 = knot(t2, i2, i3);
+    const double d01 = fmax(t1 - t0, eps), d12 = fmax(t2 - t1, eps), d23 = fmax(t3 - t2, eps);
+    const double d02 = fmax(t2 - t0, eps), d13 = fmax(t3 - t1, eps);
+    const double step = (t2 - t1) / (double)num;
+    for (int k = lane; k < num; k += kWave) {
+      const double t = (double)k * step + t1;
+      double c[2];
+      for (int d = 0; d < 2; ++d) {
+        const double p0 = pts[2 * i0 + d], p1 = pts[2 * i1 + d], p2 = pts[2 * i2 + d], p3 = pts[2 * i3 + d];
+        const double a1 = (t1 - t) / d01 * p0 + (t - t0) / d01 * p1;
+        const double a2 = (t2 - t) / d12 * p1 + (t - t1) / d12 * p2;
+        const double a3 = (t3 - t) / d23 * p2 + (t - t2) / d23 * p3;
+        const double b1 = (t2 - t) / d02 * a1 + (t - t0) / d02 * a2;
+        const double b2 = (t3 - t) / d13 * a2 + (t - t1) / d13 * a3;
+        c[d] = (t2 - t) / d12 * b1 + (t - t1) / d12 * b2;
+      }
+      out[2 * (i * num + k)] = c[0];
+      out[2 * (i * num + k) + 1] = c[1];
+    }
+  }
+  if (lane < 2) out[2 * (total - 1) + lane] = pts[2 * (n - 1) + lane];
+  return total;
+}
+
 }  // namespace

@@ -1,6 +1,6 @@
 // mpcqp_solve.h -- K2 solver kernel (setup -> ADMM -> polish), templated on the horizon N.
 #pragma once
-#include "mpcqp_common.h"
+#include "mpcqp_build.h"
 
 namespace {
 using mpcqp::Launch;
@@ -264,8 +264,10 @@ struct Ctx {
 //   slot 2: rate row         U_p - U_{p-2} (u_prev at k = 0)           (:89-106)
 // the constant parts (v_0 = x0[3], u_prev) moved into the bounds.
 template <int N>
-__device__ __forceinline__ bool setup_qp(const mpcqp_params& p, int b, const double* __restrict__ model, Ctx<N>& C,
-                                         SolveLds<N>& lds, double* __restrict__ scratch, double* __restrict__ dbg) {
+__device__ __forceinline__ bool setup_qp(const mpcqp_params& p, int b, const double* __restrict__ model,
+                                         const double* __restrict__ in_x0, const double* __restrict__ in_ref,
+                                         const double* __restrict__ in_up, Ctx<N>& C, SolveLds<N>& lds,
+                                         double* __restrict__ scratch, double* __restrict__ dbg) {
   constexpr int n = 2 * N;
   SetupSmem<N>& sm = lds.setup;
   (void)scratch;
@@ -279,7 +281,19 @@ __device__ __forceinline__ bool setup_qp(const mpcqp_params& p, int b, const dou
   T2.begin();
   T.begin();
 
-  {
+  if (in_ref) {  // K1 fused: the window -> LTV model straight into LDS (mpcqp_build.h)
+    const double* rb = in_ref + (size_t)b * (N + 1) * 4;
+    double rx = 0.0, ry = 0.0, ryaw = 0.0, rv = 0.0;
+    if (lane <= N) {
+      rx = rb[4 * lane + 0];
+      ry = rb[4 * lane + 1];
+      ryaw = rb[4 * lane + 2];
+      rv = rb[4 * lane + 3];
+    }
+    const double x0l = lane < 4 ? in_x0[(size_t)b * 4 + lane] : 0.0;
+    const double upl = (lane >= 4 && lane < 6 && in_up) ? in_up[(size_t)b * 2 + lane - 4] : 0.0;
+    build_qp(p, lane, rx, ry, ryaw, rv, x0l, upl, sm.model);
+  } else {
     const double* mb = model + (size_t)b * S;
     for (int i = lane; i < S; i += kWave) sm.model[i] = mb[i];
   }
@@ -943,7 +957,9 @@ __device__ __forceinline__ int admm_qp(const mpcqp_params& p, Ctx<N>& C, bool ba
 
 // ------------------------------------------------------------------ K2c: polish + outputs
 template <int N>
-__device__ __forceinline__ void finish_qp(const mpcqp_params& p, int b, const double* __restrict__ model, Ctx<N>& C,
+__device__ __forceinline__ void finish_qp(const mpcqp_params& p, int b, const double* __restrict__ model,
+                                          const double* __restrict__ in_x0, const double* __restrict__ in_ref,
+                                          const double* __restrict__ in_up, Ctx<N>& C,
                                           double x_in, const double z_admm[3], int admm_flag, int admm_it, int nfact,
                                           int pol_it, int n_ls, double* __restrict__ u0o, double* __restrict__ Xo,
                                           double* __restrict__ Uo, int32_t* __restrict__ statuso,
@@ -992,15 +1008,51 @@ __device__ __forceinline__ void finish_qp(const mpcqp_params& p, int b, const do
   }
 
   // ---- outputs (unscaled): speeds W -> accelerations; states by the LTV recursion ----
-  const double* mb = model + (size_t)b * model_stride(N);
+  // the model's lane values: re-derived from the inputs when K1 is fused (the LDS copy is gone)
+  double m_al = 0.0, m_be = 0.0, m_ga = 0.0, m_et = 0.0, m_si = 0.0, m_c0 = 0.0, m_c1 = 0.0;
+  double x00, x01, x02, x03, up0, up1;
+  if (in_ref) {
+    const double* rb = in_ref + (size_t)b * (N + 1) * 4;
+    const double ryaw = lane <= N ? rb[4 * lane + 2] : 0.0, rv = lane <= N ? rb[4 * lane + 3] : 0.0;
+    const LaneModel m = build_lane(p, lane, ryaw, rv);
+    m_al = m.al;
+    m_be = m.be;
+    m_ga = m.ga;
+    m_et = m.et;
+    m_si = m.si;
+    m_c0 = m.c0;
+    m_c1 = m.c1;
+    x00 = in_x0[(size_t)b * 4 + 0];
+    x01 = in_x0[(size_t)b * 4 + 1];
+    x02 = in_x0[(size_t)b * 4 + 2];
+    x03 = in_x0[(size_t)b * 4 + 3];
+    up0 = in_up ? in_up[(size_t)b * 2 + 0] : 0.0;
+    up1 = in_up ? in_up[(size_t)b * 2 + 1] : 0.0;
+  } else {
+    const double* mb = model + (size_t)b * model_stride(N);
+    if (lane < N) {
+      m_al = mb[lane];
+      m_be = mb[N + lane];
+      m_ga = mb[2 * N + lane];
+      m_et = mb[3 * N + lane];
+      m_si = mb[4 * N + lane];
+      m_c0 = mb[5 * N + lane];
+      m_c1 = mb[6 * N + lane];
+    }
+    x00 = mb[11 * N + 4];
+    x01 = mb[11 * N + 5];
+    x02 = mb[11 * N + 6];
+    x03 = mb[11 * N + 7];
+    up0 = mb[11 * N + 8];
+    up1 = mb[11 * N + 9];
+  }
   const int cc = lane & 1;
   const double W = act ? C.D * x : 0.0;  // v_{j+1} on lane 2j, delta_j on lane 2j+1
   const double dt = p.dt;
-  const double x00 = mb[11 * N + 4], x01 = mb[11 * N + 5], x02 = mb[11 * N + 6], x03 = mb[11 * N + 7];
-  const double up0 = mb[11 * N + 8], up1 = mb[11 * N + 9];
   const double Wm2 = shr2(W);
   const double U = !act ? 0.0 : (cc == 1 ? W : (W - (lane == 0 ? x03 : Wm2)) / dt);
-  const double sj = act ? mb[4 * N + (lane >> 1)] : 0.0;
+  const double sj_all = __shfl(m_si, lane >> 1, kWave);
+  const double sj = act ? sj_all : 0.0;
   // psi_{j+1} on lane 2j+1
   const double sacc = scan_add((act && cc == 1) ? sj * U : 0.0, lane);
   // lane k <- (psi_k, v_k)
@@ -1011,8 +1063,8 @@ __device__ __forceinline__ void finish_qp(const mpcqp_params& p, int b, const do
   const double pk = lane == 0 ? x02 : x02 + pk_s;
   double t0 = 0.0, t1 = 0.0;
   if (lane < N) {
-    t0 = mb[lane] * pk + mb[N + lane] * vk + mb[5 * N + lane];
-    t1 = mb[2 * N + lane] * pk + mb[3 * N + lane] * vk + mb[6 * N + lane];
+    t0 = m_al * pk + m_be * vk + m_c0;
+    t1 = m_ga * pk + m_et * vk + m_c1;
   }
   const double in0 = scan_add(t0, lane), in1 = scan_add(t1, lane);
   const double ex0 = dpp<kWaveShr1>(in0), ex1 = dpp<kWaveShr1>(in1);  // exclusive prefix
@@ -1060,7 +1112,9 @@ __device__ __forceinline__ void finish_qp(const mpcqp_params& p, int b, const do
 // its SIMD's FP64 issue with two others.
 template <int N>
 __global__ __launch_bounds__(kWave, 2) void k_solve(mpcqp_params p, int B, const uint8_t* __restrict__ mask,
-                                                 const double* __restrict__ model, double* __restrict__ state,
+                                                 const double* __restrict__ model, const double* __restrict__ in_x0,
+                                                 const double* __restrict__ in_ref, const double* __restrict__ in_up,
+                                                 double* __restrict__ state,
                                                  double* __restrict__ u0o, double* __restrict__ Xo,
                                                  double* __restrict__ Uo, int32_t* __restrict__ statuso,
                                                  int32_t* __restrict__ iterso, uint8_t* __restrict__ activeo) {
@@ -1070,11 +1124,12 @@ __global__ __launch_bounds__(kWave, 2) void k_solve(mpcqp_params p, int B, const
   double* dbg = p.debug_state ? state + (size_t)b * state_stride(N) : nullptr;
   const uint64_t t_start = __builtin_amdgcn_s_memtime();
   Ctx<N> C;
-  const bool bad = setup_qp<N>(p, b, model, C, sm, state + (size_t)b * state_stride(N), dbg);
+  const bool bad = setup_qp<N>(p, b, model, in_x0, in_ref, in_up, C, sm, state + (size_t)b * state_stride(N), dbg);
   double x = 0.0, z[3] = {0.0, 0.0, 0.0};
   int flag = bad ? -1 : 0, it = 0, nfact = 0, pol_it = 0, n_ls = 0;
   if (p.method == MPCQP_METHOD_ADMM) flag = admm_qp<N>(p, C, bad, x, z, it, nfact, pol_it, n_ls, dbg);
-  finish_qp<N>(p, b, model, C, x, z, flag, it, nfact, pol_it, n_ls, u0o, Xo, Uo, statuso, iterso, activeo);
+  finish_qp<N>(p, b, model, in_x0, in_ref, in_up, C, x, z, flag, it, nfact, pol_it, n_ls, u0o, Xo, Uo, statuso, iterso,
+               activeo);
   if (dbg && threadIdx.x == 0)  // this wave's cycles, start to finish (tools/qp_cycles.py)
     dbg[state_scal_off(N) + 4] = (double)(__builtin_amdgcn_s_memtime() - t_start);
 }
@@ -1084,7 +1139,8 @@ __global__ __launch_bounds__(kWave, 2) void k_solve(mpcqp_params p, int B, const
 namespace mpcqp {
 template <int N>
 void launch_solve(hipStream_t s, const Launch& L) {
-  hipLaunchKernelGGL(k_solve<N>, dim3(L.B), dim3(kWave), 0, s, *L.p, L.B, L.mask, L.model, L.state, L.u0, L.X, L.U,
+  hipLaunchKernelGGL(k_solve<N>, dim3(L.B), dim3(kWave), 0, s, *L.p, L.B, L.mask, L.model, L.x0, L.ref, L.u_prev,
+                     L.state, L.u0, L.X, L.U,
                      L.st, L.it, L.ac);
 }
 

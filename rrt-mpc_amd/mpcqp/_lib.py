@@ -123,6 +123,9 @@ FLEET_RUNNING = 0
 FLEET_GOAL = 1
 FLEET_ABORTED = 2
 FLEET_OUT_OF_STEPS = 3
+FLEET_REPLAN_RUNNING = 4  # transient inside mpcqp_swarm_step
+FLEET_REPLAN_ABORTED = 5
+CATMULL_MAX_POINTS = 4096  # deduplicated points per path of mpcqp_catmull_rom
 
 
 class MpcqpFleet(ctypes.Structure):
@@ -169,6 +172,41 @@ class MpcqpRrtParams(ctypes.Structure):
 RRT_MAX_ITERATIONS = 5000
 
 
+class MpcqpSwarm(ctypes.Structure):
+    """``mpcqp_swarm`` (include/mpcqp.h): replan trigger + device replanning of the config-5 swarm."""
+
+    _fields_ = [
+        ("rrt", MpcqpRrtParams),
+        ("occupancy", ctypes.c_void_p),
+        ("prune", ctypes.c_int32),
+        ("spline_samples", ctypes.c_int32),
+        ("spline_alpha", ctypes.c_double),
+        ("dedupe_tol", ctypes.c_double),
+        ("desired_speed", ctypes.c_double),
+        ("dt", ctypes.c_double),
+        ("horizon", ctypes.c_int32),
+        ("max_replans", ctypes.c_int32),
+        ("replan_distance", ctypes.c_double),
+        ("path_cap", ctypes.c_int32),
+        ("reserved", ctypes.c_int32),
+        ("rng_table", ctypes.c_void_p),
+        ("replans", ctypes.c_void_p),
+        ("replan_step", ctypes.c_void_p),
+        ("start_goal", ctypes.c_void_p),
+        ("nodes", ctypes.c_void_p),
+        ("count", ctypes.c_void_p),
+        ("meta", ctypes.c_void_p),
+        ("raw", ctypes.c_void_p),
+        ("raw_len", ctypes.c_void_p),
+        ("pruned", ctypes.c_void_p),
+        ("pruned_len", ctypes.c_void_p),
+        ("smooth", ctypes.c_void_p),
+        ("smooth_len", ctypes.c_void_p),
+        ("new_ref", ctypes.c_void_p),
+        ("new_len", ctypes.c_void_p),
+    ]
+
+
 class LibraryError(RuntimeError):
     pass
 
@@ -197,6 +235,13 @@ _SYMBOLS = {
     "mpcqp_rrt_paths": ([ctypes.POINTER(MpcqpRrtParams), ctypes.c_int, ctypes.c_int] + [ctypes.c_void_p] * 9,
                         ctypes.c_int),
     "mpcqp_inflate": ([ctypes.c_int] * 4 + [ctypes.c_void_p] * 3, ctypes.c_int),
+    "mpcqp_catmull_rom": ([ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_double,
+                           ctypes.c_double, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p],
+                          ctypes.c_int),
+    "mpcqp_swarm_step": ([ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(MpcqpFleet), ctypes.POINTER(MpcqpSwarm),
+                          ctypes.c_void_p], ctypes.c_int),
+    "mpcqp_swarm_run": ([ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(MpcqpFleet), ctypes.POINTER(MpcqpSwarm),
+                         ctypes.c_int, ctypes.c_int, ctypes.c_void_p], ctypes.c_int),
     "mpcqp_model_buffer": ([ctypes.c_void_p], ctypes.c_void_p),
     "mpcqp_model_stride": ([ctypes.c_int], ctypes.c_int),
     "mpcqp_state_buffer": ([ctypes.c_void_p], ctypes.c_void_p),
@@ -242,7 +287,11 @@ __all__ = [
     "MpcqpParams",
     "MpcqpFleet",
     "MpcqpRrtParams",
+    "MpcqpSwarm",
     "RRT_MAX_ITERATIONS",
+    "FLEET_REPLAN_RUNNING",
+    "FLEET_REPLAN_ABORTED",
+    "CATMULL_MAX_POINTS",
     "to_c_params",
     "REF_BAD_PATH",
     "REF_MAX_POINTS",

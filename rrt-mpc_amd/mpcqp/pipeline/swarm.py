@@ -1,19 +1,24 @@
-"""BASELINE config 5: a swarm of vehicles on one inflated grid, planned and tracked on the GPU.
+"""BASELINE config 5: a swarm of vehicles on one inflated grid, planned, tracked and re-planned
+on the GPU with a per-step replan trigger.
 
 ``Swarm.run`` chains the batched stages for V vehicles:
-  1. plan    -- ``BatchedRRTStarPlanner.plan_batch`` (one RRT* tree per vehicle, GPU), then the
-               reference's prune + Catmull-Rom post-processing (host);
+  1. plan    -- ``BatchedRRTStarPlanner.paths_batch``: one RRT* tree per vehicle, path extraction,
+               shortcut pruning and Catmull-Rom smoothing on the device (``rrt_star.py:201-289``);
   2. refs    -- ``build_reference_batch`` (GPU) straight into the fleet's buffers;
-  3. track   -- ``FleetTracker`` closed loop (GPU), ``check_every`` steps per host check;
-  4. replan  -- the trigger the reference lists as roadmap (``README.md:146-148``): after each
-               check, vehicles that aborted (QP unsolved after relaxation) or left their
-               reference (distance to ``ref[path_idx]`` above ``replan_distance``) are re-planned
-               together from where they stand, their references rebuilt and their loop state
-               reset (path_idx 0, phase running), at most ``max_replans`` times each.
+  3. track + replan -- ``mpcqp_swarm_run`` (``csrc/mpcqp_swarm.hip``), every step on the device:
+               the fleet closed-loop step (``control_stage.py:100-150``), then the trigger the
+               reference lists as roadmap (``README.md:146-148``) -- a vehicle farther than
+               ``replan_distance`` from ``ref[path_idx]`` after its step, or one whose QP stayed
+               unsolved after relaxation (aborted) -- and, in the same step, its replanning from
+               where it stands (RRT* with its next seed ``seed + 7919 (r + 1)``, pruning,
+               smoothing, build_reference); pose, speed and u_prev carry over, path_idx restarts at
+               0.  At most ``max_replans`` per vehicle.  The whole step is one hipGraph replay; the
+               host only polls every ``check_every`` steps whether any vehicle still runs.
 Every vehicle between replans follows the reference's single-vehicle loop exactly.
 """
 from __future__ import annotations
 
+import ctypes
 import time
 from dataclasses import dataclass, field
 from typing import Dict, List, Optional
@@ -21,9 +26,14 @@ from typing import Dict, List, Optional
 import numpy as np
 
 from .. import _lib
-from ..control.ref_builder import build_reference_batch
-from ..planning.rrt_star import BatchedRRTStarPlanner, PlannerParameters
+from ..planning.rrt_star import BatchedRRTStarPlanner, PlannerParameters, pcg64_states
 from .fleet import FleetTracker
+
+REPLAN_SEED_STRIDE = 7919  # replan r of vehicle v draws from default_rng(seed_v + 7919 (r + 1))
+
+
+def replan_seed(seed: int, r: int) -> int:
+    return int(seed) + REPLAN_SEED_STRIDE * (int(r) + 1)
 
 
 @dataclass
@@ -31,15 +41,20 @@ class SwarmResult:
     states: List[np.ndarray]  # per vehicle: states after each step, across replans
     phase: np.ndarray  # final MPCQP_FLEET_* phase
     steps: np.ndarray  # closed-loop steps per vehicle
-    replans: np.ndarray  # replans per vehicle
+    replans: np.ndarray  # replan attempts per vehicle
     planned: np.ndarray  # initial plan succeeded
+    paths: List[Optional[list]] = field(default_factory=list)  # initial plan per vehicle (None: no plan)
+    replan_steps: Optional[np.ndarray] = None  # (V, max_replans): steps[v] at replan r, -steps-1 failed, 0 unused
+    last_replan_start: Optional[np.ndarray] = None  # (V, 2): where the last replan started
+    last_replan_path: List[Optional[np.ndarray]] = field(default_factory=list)  # its final path (None: failed/none)
+    inputs: List[np.ndarray] = field(default_factory=list)  # per vehicle: applied u0 per step
     timings: Dict[str, float] = field(default_factory=dict)
 
 
 class Swarm:
     def __init__(self, occupancy: np.ndarray, mpc, planner: PlannerParameters, *, map_resolution: float,
                  max_vehicles: int, max_ref_len: int = 512, device=None, replan_distance: float = 15.0,
-                 max_replans: int = 2) -> None:
+                 max_replans: int = 2, path_cap: int = 2048, use_graph: bool = True) -> None:
         self.occupancy = np.ascontiguousarray(occupancy, dtype=np.uint8)
         self.mpc = mpc
         self.planner = BatchedRRTStarPlanner(self.occupancy, planner, device=device)
@@ -48,14 +63,68 @@ class Swarm:
         self.device = self.planner.device
         self.replan_distance = float(replan_distance)
         self.max_replans = int(max_replans)
+        self.path_cap = int(path_cap)
+        self.use_graph = bool(use_graph)
+        self._L = _lib.lib()
 
     def _plan(self, starts, goals, seeds):
-        """Final paths of every problem (growth, extraction and pruning on the device);
+        """Final paths of every problem (growth, extraction, pruning and smoothing on the device);
         returns (success mask, paths with the start alone where no plan was found)."""
-        found = self.planner.paths_batch(starts, goals, seeds)
+        found = self.planner.paths_batch(starts, goals, seeds, smoothing="device")
         ok = np.array([p is not None for p in found], dtype=bool)
         paths = [p if p is not None else [tuple(s)] for p, s in zip(found, starts)]
-        return ok, paths
+        return ok, paths, found
+
+    def _swarm_struct(self, V: int, seeds, planned) -> tuple:
+        torch = self.fleet._torch
+        dev = dict(device=self.device)
+        R = max(self.max_replans, 1)
+        M = int(self.planner.params.max_iterations) + 2
+        S = self.fleet.max_ref_len
+        table = np.zeros((max(V, 1), R, 4), dtype=np.uint64)
+        if self.max_replans:
+            for v in range(V):
+                table[v] = pcg64_states([replan_seed(seeds[v], r) for r in range(self.max_replans)])
+        f64, i32 = torch.float64, torch.int32
+        n = max(V, 1)
+        b = {
+            "rng_table": torch.from_numpy(table).to(**dev),
+            # vehicles without an initial plan never replan (the reference raises, control_stage.py:69-72)
+            "replans": torch.from_numpy(np.where(planned, 0, self.max_replans).astype(np.int32)
+                                        if V else np.zeros(1, np.int32)).to(**dev),
+            "replan_step": torch.zeros((n, R), dtype=i32, **dev),
+            "start_goal": torch.zeros((n, 4), dtype=f64, **dev),
+            "nodes": torch.zeros((n, M, 4), dtype=f64, **dev),
+            "count": torch.zeros((n,), dtype=i32, **dev),
+            "meta": torch.zeros((n, 2), dtype=i32, **dev),
+            "raw": torch.zeros((n, M, 2), dtype=f64, **dev),
+            "raw_len": torch.zeros((n,), dtype=i32, **dev),
+            "pruned": torch.zeros((n, M, 2), dtype=f64, **dev),
+            "pruned_len": torch.zeros((n,), dtype=i32, **dev),
+            "smooth": torch.zeros((n, self.path_cap, 2), dtype=f64, **dev),
+            "smooth_len": torch.zeros((n,), dtype=i32, **dev),
+            "new_ref": torch.zeros((n, S, 4), dtype=f64, **dev),
+            "new_len": torch.zeros((n,), dtype=i32, **dev),
+        }
+        occ = torch.from_numpy(self.occupancy).to(**dev)
+        s = _lib.MpcqpSwarm()
+        s.rrt = self.planner._c
+        s.occupancy = occ.data_ptr()
+        pp = self.planner.params
+        s.prune = int(bool(pp.prune_path))
+        s.spline_samples = int(pp.spline_samples)
+        s.spline_alpha = float(pp.spline_alpha)
+        s.dedupe_tol = float(pp.dedupe_tolerance)
+        s.desired_speed = float(self.mpc.v_px_s)
+        s.dt = float(self.mpc.dt)
+        s.horizon = int(self.fleet.horizon)
+        s.max_replans = self.max_replans
+        s.replan_distance = self.replan_distance
+        s.path_cap = self.path_cap
+        for k, t in b.items():
+            setattr(s, k, t.data_ptr())
+        b["occupancy"] = occ
+        return s, b
 
     def run(self, starts: np.ndarray, goals: np.ndarray, seeds=None, *, sim_steps: Optional[int] = None,
             check_every: int = 10) -> SwarmResult:
@@ -67,70 +136,46 @@ class Swarm:
         total = int(self.mpc.sim_steps if sim_steps is None else sim_steps)
         t = {}
         t0 = time.perf_counter()
-        planned, paths = self._plan(starts, goals, seeds)
+        planned, paths, found = self._plan(starts, goals, seeds)
         t["plan_s"] = time.perf_counter() - t0
         t0 = time.perf_counter()
         self.fleet.reset_from_plans(paths, starts, goals, max_steps=total, device_reference=True)
-        b = self.fleet.buffers()
+        fb = self.fleet.buffers()
         if (~planned).any():  # no plan: the vehicle never starts (the reference raises, :69-72)
-            b["phase"][torch.from_numpy(np.flatnonzero(~planned)).to(self.device)] = _lib.FLEET_ABORTED
+            fb["phase"][torch.from_numpy(np.flatnonzero(~planned)).to(self.device)] = _lib.FLEET_ABORTED
+        sw, sb = self._swarm_struct(V, seeds, planned)
         torch.cuda.synchronize(self.device)
         t["refs_s"] = time.perf_counter() - t0
-        replans = np.zeros(V, dtype=np.int64)
-        t_track = t_replan = 0.0
+        t0 = time.perf_counter()
+        stream = torch.cuda.current_stream(self.device)
         done = 0
-        while done < total:
-            t0 = time.perf_counter()
+        while done < total and V:
             k = min(check_every, total - done)
-            self.fleet.step(k)
+            _lib.check(self._L.mpcqp_swarm_run(self.fleet._nominal._ws, self.fleet._relaxed._ws,
+                                               ctypes.byref(self.fleet._fleet), ctypes.byref(sw), int(k),
+                                               int(self.use_graph), ctypes.c_void_p(stream.cuda_stream)),
+                       "mpcqp_swarm_run")
             done += k
-            phase = b["phase"][:V].cpu().numpy()
-            t_track += time.perf_counter() - t0
-            if not (phase == _lib.FLEET_RUNNING).any() and not self._any_replannable(phase, replans, planned):
+            if not bool((fb["phase"][:V] == _lib.FLEET_RUNNING).any().item()):
                 break
-            t0 = time.perf_counter()
-            need = self._replan_candidates(phase, replans, planned)
-            if len(need):
-                self._replan(need, goals, seeds, replans)
-            t_replan += time.perf_counter() - t0
-        t["track_s"] = t_track
-        t["replan_s"] = t_replan
+        torch.cuda.synchronize(self.device)
+        t["track_replan_s"] = time.perf_counter() - t0
         r = self.fleet.result()
-        return SwarmResult(states=r.states, phase=r.phase, steps=r.steps, replans=replans, planned=planned, timings=t)
-
-    def _any_replannable(self, phase, replans, planned) -> bool:
-        return bool(((phase == _lib.FLEET_ABORTED) & planned & (replans < self.max_replans)).any())
-
-    def _replan_candidates(self, phase, replans, planned) -> np.ndarray:
-        b = self.fleet.buffers()
-        V = len(phase)
-        state = b["state"][:V].cpu().numpy()
-        pidx = b["path_idx"][:V].long()
-        ref_pt = b["ref_global"][:V].gather(1, pidx.view(-1, 1, 1).expand(-1, 1, 4)).squeeze(1).cpu().numpy()
-        off = np.hypot(state[:, 0] - ref_pt[:, 0], state[:, 1] - ref_pt[:, 1]) > self.replan_distance
-        trig = ((phase == _lib.FLEET_ABORTED) | ((phase == _lib.FLEET_RUNNING) & off))
-        return np.flatnonzero(trig & planned & (replans < self.max_replans))
-
-    def _replan(self, idx: np.ndarray, goals, seeds, replans) -> None:
-        torch = self.fleet._torch
-        b = self.fleet.buffers()
-        state = b["state"][:len(replans)].cpu().numpy()
-        starts = state[idx, :2]
-        ok, paths = self._plan(starts, goals[idx], seeds[idx] + 7919 * (replans[idx] + 1))
-        replans[idx] += 1
-        if not ok.any():
-            return
-        sel = idx[ok]
-        ref, ref_len = build_reference_batch([paths[i] for i in np.flatnonzero(ok)], self.mpc.v_px_s,
-                                             self.fleet.horizon, self.mpc.dt, device=self.device,
-                                             ref_stride=self.fleet.max_ref_len)
-        if (ref_len < 1).any():
-            raise ValueError("replanned reference exceeds max_ref_len")
-        si = torch.from_numpy(sel).to(self.device)
-        b["ref_global"][si] = ref
-        b["ref_len"][si] = ref_len
-        b["path_idx"][si] = 0
-        b["phase"][si] = _lib.FLEET_RUNNING  # pose, speed and u_prev carry over
+        replans = sb["replans"][:V].cpu().numpy().astype(np.int64)
+        replans = np.where(planned, replans, 0)
+        rsteps = sb["replan_step"][:V, : max(self.max_replans, 1)].cpu().numpy()
+        sg = sb["start_goal"][:V].cpu().numpy()
+        sl = sb["smooth_len"][:V].cpu().numpy()
+        smooth = sb["smooth"][:V].cpu().numpy()
+        last_paths = []
+        for v in range(V):
+            if replans[v] and rsteps[v, replans[v] - 1] >= 0 and sl[v] >= 1:
+                last_paths.append(smooth[v, : sl[v]].copy())
+            else:
+                last_paths.append(None)
+        return SwarmResult(states=r.states, phase=r.phase, steps=r.steps, replans=replans, planned=planned,
+                           paths=found, replan_steps=rsteps, last_replan_start=sg[:, :2].copy(),
+                           last_replan_path=last_paths, inputs=r.inputs, timings=t)
 
 
-__all__ = ["Swarm", "SwarmResult"]
+__all__ = ["Swarm", "SwarmResult", "replan_seed", "REPLAN_SEED_STRIDE"]

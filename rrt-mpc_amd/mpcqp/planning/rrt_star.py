@@ -265,18 +265,43 @@ class BatchedRRTStarPlanner:
                                                   ctypes.c_void_p(stream.cuda_stream)), "mpcqp_rrt_paths")
         return raw[:V], raw_len[:V], pruned[:V], pruned_len[:V]
 
-    def paths_batch(self, starts, goals, seeds=None) -> List[Optional[List[Tuple[float, float]]]]:
+    def smooth(self, paths, lens, stream=None, *, out_stride: int = 4096):
+        """Centripetal Catmull-Rom of device paths ``paths`` (V, stride, 2) with ``lens`` (V,) points on
+        the device (``mpcqp_catmull_rom``, ``rrt_star.py:104-159``); returns (out (V, out_stride, 2),
+        out_len (V,)) device tensors (out_len -1: over capacity)."""
+        torch = self._torch
+        V = int(paths.shape[0])
+        out = torch.empty((max(V, 1), out_stride, 2), dtype=torch.float64, device=self.device)
+        out_len = torch.empty((max(V, 1),), dtype=torch.int32, device=self.device)
+        if stream is None:
+            stream = torch.cuda.current_stream(self.device)
+        paths = paths.contiguous()
+        lens = lens.to(torch.int32).contiguous()
+        with torch.cuda.device(self.device):
+            _lib.check(_lib.lib().mpcqp_catmull_rom(V, paths.data_ptr(), lens.data_ptr(), int(paths.shape[1]),
+                                                    int(self.params.spline_samples), float(self.params.spline_alpha),
+                                                    float(self.params.dedupe_tolerance), out.data_ptr(),
+                                                    out_len.data_ptr(), int(out_stride),
+                                                    ctypes.c_void_p(stream.cuda_stream)), "mpcqp_catmull_rom")
+        return out[:V], out_len[:V]
+
+    def paths_batch(self, starts, goals, seeds=None, *, smoothing: str = "host"
+                    ) -> List[Optional[List[Tuple[float, float]]]]:
         """The final path of ``plan(start, goal)`` for every problem (None where no goal was
         reached), without building the tree on the host: growth, extraction and pruning run on
-        the device; only the pruned paths come back for the Catmull-Rom smoothing
-        (``rrt_star.py:264-283``).  Equal to ``plan_batch(...)[v].path``."""
+        the device; the Catmull-Rom smoothing (``rrt_star.py:264-283``) on the host from the
+        pruned paths (``smoothing="host"``: equal to ``plan_batch(...)[v].path`` bit for bit) or on
+        the device (``smoothing="device"``: within the ~1e-5 px that the reference's duplicated
+        end points amplify an ulp to)."""
         starts = np.asarray(starts, dtype=float).reshape(-1, 2)
         V = len(starts)
         if seeds is None:
             seeds = [self.params.random_seed] * V
         nodes, count, meta = self.grow(starts, goals, seeds)
-        _, _, pruned, plen = self.extract(nodes, count, meta)
-        plen = plen.cpu().numpy()
+        _, _, pruned, plen_t = self.extract(nodes, count, meta)
+        if smoothing == "device" and V:
+            return self._device_final_paths(pruned, plen_t)
+        plen = plen_t.cpu().numpy()
         L = int(plen.max()) if V else 0
         pts = pruned[:, :L].cpu().numpy()
         out: List[Optional[List[Tuple[float, float]]]] = []
@@ -292,6 +317,30 @@ class BatchedRRTStarPlanner:
                 if len(spline) >= 2:
                     working = [tuple(map(float, pt)) for pt in spline]
             out.append(working)
+        return out
+
+    def _device_final_paths(self, pruned, plen_t) -> List[Optional[List[Tuple[float, float]]]]:
+        """rrt_star.py:264-283 with the smoothing on the device: the smoothed path when
+        spline_samples > 1 and it has >= 2 points, else the pruned path."""
+        plen = plen_t.cpu().numpy()
+        smooth = self.params.spline_samples > 1
+        if smooth:
+            Lp = int(plen.max())
+            sm, sl = self.smooth(pruned[:, :max(Lp, 1)], plen_t,
+                                 out_stride=max(2, (max(Lp, 1) - 1) * max(2, self.params.spline_samples + 1) + 1))
+            sl = sl.cpu().numpy()
+            Ls = int(max(sl.max(), 1))
+            sm = sm[:, :Ls].cpu().numpy()
+        pts = pruned[:, :max(int(plen.max()), 1)].cpu().numpy()
+        out: List[Optional[List[Tuple[float, float]]]] = []
+        for v in range(len(plen)):
+            n = int(plen[v])
+            if n == 0:
+                out.append(None)
+            elif smooth and n >= 2 and sl[v] >= 2:
+                out.append([tuple(map(float, q)) for q in sm[v, : sl[v]]])
+            else:
+                out.append([tuple(map(float, q)) for q in pts[v, :n]])
         return out
 
     def plan_batch(self, starts, goals, seeds=None, *, samples=None) -> List[PlanResult]:

@@ -114,7 +114,9 @@ def test_k1_model_matches_restatement(cuda):
     ref[::3, 7:, 2] += 2 * np.pi
     ref[1::3, 12:, 2] -= 4 * np.pi
     params = _params(20)
-    ctrl = BatchedMPCController(params, 256, device="cuda:0")
+    # debug_state: K1 runs as its own kernel and leaves the model in the workspace (otherwise it
+    # is fused into the solve and never leaves the CU)
+    ctrl = BatchedMPCController(params, 256, device="cuda:0", debug_state=1)
     ctrl.solve_batch(batch.x0, ref, batch.u_prev)
     torch.cuda.synchronize()
     S = _lib.lib().mpcqp_model_stride(20)
@@ -151,7 +153,7 @@ def test_k1_unwrap_golden_exact_pi(cuda, golden):
         ref[:, :, 0] = np.arange(n)
         ref[:, :, 2] = g["p"][case, :n]
         ref[:, :, 3] = 10.0
-        ctrl = BatchedMPCController(_params(N), 2, device="cuda:0")
+        ctrl = BatchedMPCController(_params(N), 2, device="cuda:0", debug_state=1)
         ctrl.solve_batch(np.zeros((2, 4)), ref, np.zeros((2, 2)))
         torch.cuda.synchronize()
         S = _lib.lib().mpcqp_model_stride(N)
@@ -161,6 +163,19 @@ def test_k1_unwrap_golden_exact_pi(cuda, golden):
         assert np.array_equal(yaw[0], g["unwrapped"][case, :n]), case
         assert np.array_equal(yaw[1], g["unwrapped"][case, :n]), case
         ctrl.close()
+
+
+def test_fused_k1_equals_separate_k1(cuda):
+    """K1 fused into k_solve (the default: the model never leaves the CU) and K1 as its own kernel
+    through the model buffer (debug_state) give the same bits for every output."""
+    from mpcqp import scenarios
+
+    batch = scenarios.config3(256)
+    params = _params(20)
+    a = _solve(params, batch.x0, batch.ref, batch.u_prev)
+    b = _solve(params, batch.x0, batch.ref, batch.u_prev, debug_state=1)
+    for k in ("u0", "X", "U", "status", "iters", "active"):
+        assert np.array_equal(a[k], b[k]), k
 
 
 @pytest.mark.parametrize("N", [1, 2, 5, 10, 15, 31])

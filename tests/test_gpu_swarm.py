@@ -1,9 +1,11 @@
-"""GPU tests of the config-5 swarm (mpcqp/pipeline/swarm.py): batched RRT* plans, device
-references, fleet closed loop and the replan trigger, end to end on the default inflated grid.
+"""GPU tests of the config-5 swarm (mpcqp/pipeline/swarm.py, csrc/mpcqp_swarm.hip): batched RRT*
+plans, device references, the fleet closed loop and the PER-STEP device replan trigger with the
+replanning itself on the device, end to end on the default inflated grid.
 
 Between replans every vehicle follows the reference's single-vehicle loop: a vehicle that was
-never replanned reproduces TrajectoryTracker.track on its own plan (1e-7 px), and its plan is
-the reference planner's (RRTStarPlanner with that vehicle's seed)."""
+never replanned reproduces TrajectoryTracker.track on its own plan (1e-7 px); a replanned vehicle
+reproduces it up to the replan step, its new plan is RRTStarPlanner's from where it stood with its
+replan seed, and after the replan it reproduces the reference loop body on the new reference."""
 from __future__ import annotations
 
 from types import SimpleNamespace
@@ -12,6 +14,8 @@ import numpy as np
 import pytest
 
 pytestmark = pytest.mark.gpu
+
+N_HORIZON = 15
 
 
 def _pairs(occ, V, seed):
@@ -26,54 +30,158 @@ def _pairs(occ, V, seed):
     return np.array(starts), np.array(goals)
 
 
+def _planner_params(seed=13):
+    from mpcqp.planning.rrt_star import default_planner_parameters
+
+    return default_planner_parameters(max_iterations=1500, random_seed=int(seed))
+
+
 def _swarm(occ, V, sim_steps, **kw):
     from mpcqp.config import MPCConfig
     from mpcqp.pipeline.swarm import Swarm
-    from mpcqp.planning.rrt_star import default_planner_parameters
 
-    return Swarm(occ, MPCConfig(horizon=15, sim_steps=sim_steps), default_planner_parameters(max_iterations=1500),
+    return Swarm(occ, MPCConfig(horizon=N_HORIZON, sim_steps=sim_steps), _planner_params(),
                  map_resolution=0.8, max_vehicles=V, device="cuda:0", **kw)
+
+
+def _host_track(path, start, goal, steps):
+    """TrajectoryTracker.track (control_stage.py:58-157) on one plan, B=1 GPU solves."""
+    from mpcqp.config import MPCConfig, VizConfig
+    from mpcqp.pipeline.control_stage import TrajectoryTracker
+
+    tr = TrajectoryTracker(MPCConfig(horizon=N_HORIZON, sim_steps=steps), VizConfig())
+    res = tr.track(SimpleNamespace(plan=SimpleNamespace(success=True, path=path)),
+                   SimpleNamespace(start=tuple(start), goal=tuple(goal)), map_resolution=0.8, visualize=False)
+    return np.asarray(res.states)
+
+
+def _host_continue(state, u_prev, path, goal, steps):
+    """The loop body of control_stage.py:100-150 from a given state / u_prev on a new plan (the
+    swarm's replan: pose, speed and u_prev carry over, path_idx restarts at 0)."""
+    from mpcqp.config import MPCConfig, VizConfig
+    from mpcqp.control.ref_builder import build_reference
+    from mpcqp.pipeline.control_stage import TrajectoryTracker, window_at
+
+    mpc = MPCConfig(horizon=N_HORIZON, sim_steps=steps)
+    tr = TrajectoryTracker(mpc, VizConfig())
+    params = mpc.to_parameters(0.8)
+    ref = build_reference(path, mpc.v_px_s, N_HORIZON, mpc.dt)
+    out, path_idx = [], 0
+    for _ in range(steps):
+        nxt, u0, _ = tr.step(state, window_at(ref, path_idx, N_HORIZON), u_prev, params)
+        if nxt is None:
+            break
+        state, u_prev = nxt, u0
+        out.append(state.copy())
+        if path_idx < len(ref) - 2:
+            dx, dy = state[0] - ref[path_idx][0], state[1] - ref[path_idx][1]
+            if dx * dx + dy * dy > 25.0:
+                path_idx += 1
+        if np.hypot(state[0] - goal[0], state[1] - goal[1]) < 8.0:
+            break
+    return np.asarray(out)
+
+
+def _check_plan(occ, start, goal, seed, path, tol=1e-4):
+    """The device plan against the reference planner's (RRTStarPlanner, host smoothing): same
+    number of points, coordinates within the ~1e-5 px the duplicated end knots amplify an ulp to."""
+    from mpcqp.planning.rrt_star import RRTStarPlanner
+
+    plan = RRTStarPlanner(occ, _planner_params(seed)).plan(tuple(start), tuple(goal))
+    assert plan.success
+    ref = np.asarray(plan.path)
+    got = np.asarray(path)
+    assert ref.shape == got.shape, (ref.shape, got.shape)
+    np.testing.assert_allclose(got, ref, rtol=0, atol=tol)
+
+
+def test_device_smoothing_matches_reference_planner(cuda, golden):
+    """mpcqp_catmull_rom (via paths_batch(smoothing="device")) against the host restatement of
+    rrt_star.py:104-159 on 48 plans, and on the reference's own default plan."""
+    from mpcqp.common.geometry import catmull_rom_spline
+    from mpcqp.planning.rrt_star import BatchedRRTStarPlanner
+
+    occ = golden("default_plan.npz")["occupancy"]
+    starts, goals = _pairs(occ, 48, 3)
+    pl = BatchedRRTStarPlanner(occ, _planner_params(), device="cuda:0")
+    dev = pl.paths_batch(starts, goals, np.arange(48), smoothing="device")
+    host = pl.paths_batch(starts, goals, np.arange(48), smoothing="host")
+    assert sum(p is not None for p in dev) > 40
+    for d, h in zip(dev, host):
+        assert (d is None) == (h is None)
+        if d is not None:
+            assert len(d) == len(h)
+            np.testing.assert_allclose(np.asarray(d), np.asarray(h), rtol=0, atol=1e-4)
+    # edge cases: two points, duplicates (dedupe), collinear, a single point
+    import torch
+
+    cases = [[(0.0, 0.0), (10.0, 5.0)], [(0.0, 0.0), (0.0, 0.0), (3.0, 4.0), (3.0, 4.0), (9.0, 1.0)],
+             [(0.0, 0.0), (1.0, 1.0), (2.0, 2.0), (5.0, 5.0)], [(7.0, 7.0)]]
+    W = max(len(c) for c in cases)
+    arr = np.zeros((len(cases), W, 2))
+    for i, c in enumerate(cases):
+        arr[i, : len(c)] = c
+    out, n = pl.smooth(torch.from_numpy(arr).to(cuda), torch.tensor([len(c) for c in cases], device=cuda))
+    out, n = out.cpu().numpy(), n.cpu().numpy()
+    for i, c in enumerate(cases):
+        ref = catmull_rom_spline(c, samples_per_segment=20, alpha=0.5)
+        assert n[i] == len(ref), (i, n[i], len(ref))
+        np.testing.assert_allclose(out[i, : n[i]], ref, rtol=0, atol=1e-9)
 
 
 def test_swarm_vehicles_follow_the_reference_loop(cuda, golden):
     from mpcqp import _lib
-    from mpcqp.config import MPCConfig, VizConfig
-    from mpcqp.pipeline.control_stage import TrajectoryTracker
-    from mpcqp.planning.rrt_star import RRTStarPlanner, default_planner_parameters
 
     occ = golden("default_plan.npz")["occupancy"]
     V, steps = 24, 120
     starts, goals = _pairs(occ, V, 1)
-    sw = _swarm(occ, V, steps, replan_distance=1e9)  # no replans: the plain per-vehicle loop
+    sw = _swarm(occ, V, steps, replan_distance=1e9)  # no off-track replans: the plain per-vehicle loop
     res = sw.run(starts, goals, seeds=np.arange(V), check_every=20)
     assert (res.replans == 0).all()
     assert res.planned.mean() > 0.8
-    tracker = TrajectoryTracker(MPCConfig(horizon=15, sim_steps=steps), VizConfig())
-    for v in np.flatnonzero(res.planned)[:6]:
-        plan = RRTStarPlanner(occ, default_planner_parameters(max_iterations=1500, random_seed=int(v))).plan(
-            tuple(starts[v]), tuple(goals[v]))
-        assert plan.success
-        host = np.asarray(tracker.track(SimpleNamespace(plan=plan), SimpleNamespace(start=tuple(starts[v]),
-                                        goal=tuple(goals[v])), map_resolution=0.8, visualize=False).states)
+    for v in np.flatnonzero(res.planned)[:8]:
+        host = _host_track(res.paths[v], starts[v], goals[v], steps)
         assert res.steps[v] == len(host)
         np.testing.assert_allclose(res.states[v], host, rtol=0, atol=1e-7)
+        _check_plan(occ, starts[v], goals[v], v, res.paths[v])
     done = res.phase[res.planned]
     assert np.isin(done, [_lib.FLEET_GOAL, _lib.FLEET_OUT_OF_STEPS]).all()
 
 
-def test_replan_trigger(cuda, golden):
-    """A tight off-track threshold forces replans: replanned vehicles get a fresh reference
-    from where they stand and keep tracking; every vehicle ends in a terminal phase or runs on."""
+def test_per_step_replan_100_vehicles(cuda, golden):
+    """BASELINE config 5 at its size: 100 vehicles on the default inflated grid, the trigger
+    evaluated on the device after EVERY step.  Every never-replanned vehicle equals
+    TrajectoryTracker.track on its own plan; every replanned vehicle equals it up to its replan
+    step, its new plan is the reference planner's from where it stood with its replan seed, and
+    from there it follows the reference loop body on the new reference."""
     from mpcqp import _lib
+    from mpcqp.pipeline.swarm import replan_seed
 
     occ = golden("default_plan.npz")["occupancy"]
-    V = 32
-    starts, goals = _pairs(occ, V, 2)
-    sw = _swarm(occ, V, 150, replan_distance=4.0, max_replans=2)
-    res = sw.run(starts, goals, seeds=np.arange(V), check_every=10)
-    assert res.replans.sum() > 0
-    assert (res.replans <= 2).all()
+    V, steps = 100, 150
+    starts, goals = _pairs(occ, V, 7)
+    sw = _swarm(occ, V, steps, replan_distance=5.5, max_replans=1)
+    res = sw.run(starts, goals, seeds=np.arange(V), check_every=25)
+    replanned = np.flatnonzero(res.replans > 0)
+    assert len(replanned) > 0, "the trigger never fired"
+    assert res.planned.sum() >= 90
+    ok_replans = [v for v in replanned if res.replan_steps[v, 0] > 0]
+    assert ok_replans, "no replan produced a new plan"
+    for v in np.flatnonzero(res.planned & (res.replans == 0)):
+        host = _host_track(res.paths[v], starts[v], goals[v], steps)
+        assert res.steps[v] == len(host), v
+        np.testing.assert_allclose(res.states[v], host, rtol=0, atol=1e-7)
+    for v in ok_replans[:12]:
+        s = int(res.replan_steps[v, 0])  # steps taken when the replan committed
+        host = _host_track(res.paths[v], starts[v], goals[v], s)
+        np.testing.assert_allclose(res.states[v][:s], host[:s], rtol=0, atol=1e-7)
+        start = res.last_replan_start[v]
+        np.testing.assert_array_equal(start, res.states[v][s - 1][:2])  # planned from where it stood
+        _check_plan(occ, start, goals[v], replan_seed(v, 0), res.last_replan_path[v])
+        cont = _host_continue(res.states[v][s - 1], res.inputs[v][s - 1], res.last_replan_path[v], goals[v],
+                              int(res.steps[v]) - s)
+        assert len(cont) == int(res.steps[v]) - s, v
+        np.testing.assert_allclose(res.states[v][s:], cont, rtol=0, atol=1e-6)
     reached = res.phase == _lib.FLEET_GOAL
-    assert reached.sum() >= 0.5 * res.planned.sum()
     for v in np.flatnonzero(reached):  # goal test of control_stage.py:147-150 on the last state
         assert np.hypot(*(res.states[v][-1, :2] - goals[v])) < 8.0

@@ -41,7 +41,7 @@ def test_library_exports_every_header_symbol():
 
 
 @pytest.mark.parametrize("cls_name,c_name", [("MpcqpParams", "mpcqp_params"), ("MpcqpFleet", "mpcqp_fleet"),
-                                             ("MpcqpRrtParams", "mpcqp_rrt_params")])
+                                             ("MpcqpRrtParams", "mpcqp_rrt_params"), ("MpcqpSwarm", "mpcqp_swarm")])
 def test_struct_layout_matches_c(tmp_path, cls_name, c_name):
     """ctypes mirrors of mpcqp_params / mpcqp_fleet == the C compiler's layout (sizeof, offsets)."""
     from mpcqp import _lib
