@@ -75,11 +75,13 @@ def qp_flops(N: int, iters: np.ndarray, scaling: int = 10, check: int = 25) -> n
 
 
 # ------------------------------------------------------------------ workload + sharding
-def make_global_batch(config: str, total: int):
+def make_global_batch(config: str, total: int, horizon: int = 0):
     from mpcqp import scenarios
 
     if config not in scenarios.CONFIGS:
         raise SystemExit(f"unknown config {config}")
+    if horizon:  # development / long-horizon lines: the config's generator at another N
+        return scenarios.CONFIGS[config](total, horizon=horizon)
     return scenarios.CONFIGS[config](total)
 
 
@@ -368,6 +370,7 @@ def main() -> int:
     ap.add_argument("--batch", type=int, default=0, help="QPs per GPU, weak scaling (default: the config's)")
     ap.add_argument("--global-batch", type=int, default=0,
                     help="strong scaling: a fixed global batch split over the ranks (e.g. 16384 for config 4)")
+    ap.add_argument("--horizon", type=int, default=0, help="the config's generator at another horizon N")
     ap.add_argument("--method", default="admm", choices=["admm", "newton"])
     ap.add_argument("--polish-from", type=int, default=None,
                     help="ADMM iteration of the first early polish attempt (default: the library's; 0 = off)")
@@ -395,7 +398,7 @@ def main() -> int:
     strong = args.global_batch > 0
     per_gpu = args.batch or DEFAULT_BATCH[args.config]
     total = args.global_batch if strong else per_gpu * world
-    batch = make_global_batch(args.config, total)
+    batch = make_global_batch(args.config, total, args.horizon)
     N, name = batch.horizon, batch.name
     lo, hi = shard_bounds(total, world, rank)
     counts = shard_counts(total, world)

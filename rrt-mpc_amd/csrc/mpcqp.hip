@@ -17,6 +17,12 @@
 #include "mpcqp_solve.h"  // development builds: one horizon, one translation unit
 #endif
 
+// development: the first horizon of the long-horizon kernel (A/B builds only; the product uses
+// MPCQP_WIDE_MIN_HORIZON)
+#ifndef MPCQP_WIDE_FROM
+#define MPCQP_WIDE_FROM MPCQP_WIDE_MIN_HORIZON
+#endif
+
 namespace {
 using mpcqp::Launch;
 
@@ -77,7 +83,7 @@ const mpcqp::launcher_t kLaunchers[MPCQP_WIDE_MIN_HORIZON] = {
 // per-QP doubles of the solver state buffer (debug state of the one-wave kernel, the workspace
 // of the long-horizon kernel)
 size_t ws_state_stride(int N) {
-  return N >= MPCQP_WIDE_MIN_HORIZON ? mpcqp::wide_stride(N) : (size_t)state_stride(N);
+  return N >= MPCQP_WIDE_FROM ? mpcqp::wide_stride(N) : (size_t)state_stride(N);
 }
 
 thread_local std::string g_err;
@@ -107,7 +113,7 @@ int fail(int code, const std::string& msg) {
   return code;
 }
 launcher_t launcher(int horizon) {
-  if (horizon >= MPCQP_WIDE_MIN_HORIZON && horizon <= MPCQP_MAX_HORIZON) return &launch_solve_wide;
+  if (horizon >= MPCQP_WIDE_FROM && horizon <= MPCQP_MAX_HORIZON) return &launch_solve_wide;
   return horizon >= 1 && horizon < MPCQP_WIDE_MIN_HORIZON ? kLaunchers[horizon] : nullptr;
 }
 }  // namespace mpcqp
@@ -178,7 +184,7 @@ int mpcqp_build(mpcqp_ws* ws, int B, const double* x0, const double* ref, const 
   if (B == 0) return MPCQP_OK;
   // The one-wave solve builds the model itself (K1 fused into k_solve: the model block never
   // touches HBM); the K1 kernel runs only for the long-horizon solve and for inspection builds.
-  if (ws->p.horizon < MPCQP_WIDE_MIN_HORIZON && !ws->p.debug_state) {
+  if (ws->p.horizon < MPCQP_WIDE_FROM && !ws->p.debug_state) {
     ws->in_x0 = x0;
     ws->in_ref = ref;
     ws->in_up = u_prev;

@@ -5,11 +5,20 @@
 namespace {
 using mpcqp::Launch;
 
+// The model block stays in LDS for the outputs (finish_qp) while Pbar is live, where that costs no
+// occupancy (8 workgroups of Pbar + model fit a CU's 160 KB of LDS: N <= 23); past that, the model shares
+// the setup's union with Pbar and the outputs re-derive it (K1 fused) or re-read it (workspace).
+#ifndef MPCQP_MODEL_KEEP  // development switch (A/B builds): 0 never keeps the model in LDS
+#define MPCQP_MODEL_KEEP 1
+#endif
+template <int N>
+constexpr bool kModelKept = MPCQP_MODEL_KEEP && 32 * N * N + 8 * model_stride(N) <= 163840 / 8;
+
 template <int N>
 struct SetupSmem {
   static constexpr int n = 2 * N;
   double buf[kWave];
-  double model[model_stride(N)];
+  double model[kModelKept<N> ? 1 : model_stride(N)];
   double pre[4][N + 1];  // prefix sums of alpha, beta, gamma, eta
   double err[N + 1][4];  // free-response tracking error e_m = sx_m - r_m
   double g[n];
@@ -21,9 +30,13 @@ struct SolveSmem {
 };
 
 template <int N>
-union SolveLds {
-  SetupSmem<N> setup;
-  SolveSmem<N> solve;  // setup_qp writes Pbar when its own LDS data is dead
+struct SolveLds {
+  union {
+    SetupSmem<N> setup;
+    SolveSmem<N> solve;  // setup_qp writes Pbar when its own LDS data is dead
+  };
+  double model[kModelKept<N> ? model_stride(N) : 1];  // the model block, live to the end (kModelKept)
+  __device__ double* model_ptr() { return kModelKept<N> ? model : setup.model; }
 };
 
 // ------------------------------------------------------------------ shared solver context
@@ -292,26 +305,28 @@ __device__ __forceinline__ bool setup_qp(const mpcqp_params& p, int b, const dou
     }
     const double x0l = lane < 4 ? in_x0[(size_t)b * 4 + lane] : 0.0;
     const double upl = (lane >= 4 && lane < 6 && in_up) ? in_up[(size_t)b * 2 + lane - 4] : 0.0;
-    build_qp(p, lane, rx, ry, ryaw, rv, x0l, upl, sm.model);
+    build_qp(p, lane, rx, ry, ryaw, rv, x0l, upl, lds.model_ptr());
   } else {
     const double* mb = model + (size_t)b * S;
-    for (int i = lane; i < S; i += kWave) sm.model[i] = mb[i];
+    double* md = lds.model_ptr();
+    for (int i = lane; i < S; i += kWave) md[i] = mb[i];
   }
   __syncthreads();
-  const double* al = sm.model;
-  const double* be = sm.model + N;
-  const double* ga = sm.model + 2 * N;
-  const double* et = sm.model + 3 * N;
-  const double* si = sm.model + 4 * N;
-  const double* c0 = sm.model + 5 * N;
-  const double* c1 = sm.model + 6 * N;
-  const double* rr = sm.model + 7 * N;
-  const double* x0 = sm.model + 11 * N + 4;
-  const double* up = sm.model + 11 * N + 8;
+  const double* mdl = lds.model_ptr();
+  const double* al = mdl;
+  const double* be = mdl + N;
+  const double* ga = mdl + 2 * N;
+  const double* et = mdl + 3 * N;
+  const double* si = mdl + 4 * N;
+  const double* c0 = mdl + 5 * N;
+  const double* c1 = mdl + 6 * N;
+  const double* rr = mdl + 7 * N;
+  const double* x0 = mdl + 11 * N + 4;
+  const double* up = mdl + 11 * N + 8;
 
   // prefix sums (lanes 0..3, one array each) and free response (lane 4)
   if (lane < 4) {
-    const double* a = sm.model + lane * N;
+    const double* a = mdl + lane * N;
     double acc = 0.0;
     sm.pre[lane][0] = 0.0;
     for (int k = 0; k < N; ++k) {
@@ -959,7 +974,7 @@ __device__ __forceinline__ int admm_qp(const mpcqp_params& p, Ctx<N>& C, bool ba
 template <int N>
 __device__ __forceinline__ void finish_qp(const mpcqp_params& p, int b, const double* __restrict__ model,
                                           const double* __restrict__ in_x0, const double* __restrict__ in_ref,
-                                          const double* __restrict__ in_up, Ctx<N>& C,
+                                          const double* __restrict__ in_up, const double* kept_model, Ctx<N>& C,
                                           double x_in, const double z_admm[3], int admm_flag, int admm_it, int nfact,
                                           int pol_it, int n_ls, double* __restrict__ u0o, double* __restrict__ Xo,
                                           double* __restrict__ Uo, int32_t* __restrict__ statuso,
@@ -1011,7 +1026,24 @@ __device__ __forceinline__ void finish_qp(const mpcqp_params& p, int b, const do
   // the model's lane values: re-derived from the inputs when K1 is fused (the LDS copy is gone)
   double m_al = 0.0, m_be = 0.0, m_ga = 0.0, m_et = 0.0, m_si = 0.0, m_c0 = 0.0, m_c1 = 0.0;
   double x00, x01, x02, x03, up0, up1;
-  if (in_ref) {
+  if (kModelKept<N>) {  // the model block is still in LDS
+    const double* mb = kept_model;
+    if (lane < N) {
+      m_al = mb[lane];
+      m_be = mb[N + lane];
+      m_ga = mb[2 * N + lane];
+      m_et = mb[3 * N + lane];
+      m_si = mb[4 * N + lane];
+      m_c0 = mb[5 * N + lane];
+      m_c1 = mb[6 * N + lane];
+    }
+    x00 = mb[11 * N + 4];
+    x01 = mb[11 * N + 5];
+    x02 = mb[11 * N + 6];
+    x03 = mb[11 * N + 7];
+    up0 = mb[11 * N + 8];
+    up1 = mb[11 * N + 9];
+  } else if (in_ref) {
     const double* rb = in_ref + (size_t)b * (N + 1) * 4;
     const double ryaw = lane <= N ? rb[4 * lane + 2] : 0.0, rv = lane <= N ? rb[4 * lane + 3] : 0.0;
     const LaneModel m = build_lane(p, lane, ryaw, rv);
@@ -1110,8 +1142,17 @@ __device__ __forceinline__ void finish_qp(const mpcqp_params& p, int b, const do
 // registers for a third wave (168, fits the ~13 KB of LDS at N = 20) measured no faster at
 // B = 4096: the four QPs per SIMD then run in 1.33 rounds instead of 2, but each wave shares
 // its SIMD's FP64 issue with two others.
+// From N = 29 on the KKT inverse (2N doubles per lane) leaves 2 waves per SIMD no registers for
+// the rest of the working set, and Pbar (32 N^2 bytes of LDS) already limits a CU to 5
+// workgroups: the kernel takes the register file of 1 wave per SIMD instead of spilling.
+#ifndef MPCQP_ONE_WAVE_FROM
+#define MPCQP_ONE_WAVE_FROM 29
+#endif
 template <int N>
-__global__ __launch_bounds__(kWave, 2) void k_solve(mpcqp_params p, int B, const uint8_t* __restrict__ mask,
+constexpr int kSolveWavesPerEU = N >= MPCQP_ONE_WAVE_FROM ? 1 : 2;
+
+template <int N>
+__global__ __launch_bounds__(kWave, kSolveWavesPerEU<N>) void k_solve(mpcqp_params p, int B, const uint8_t* __restrict__ mask,
                                                  const double* __restrict__ model, const double* __restrict__ in_x0,
                                                  const double* __restrict__ in_ref, const double* __restrict__ in_up,
                                                  double* __restrict__ state,
@@ -1128,7 +1169,7 @@ __global__ __launch_bounds__(kWave, 2) void k_solve(mpcqp_params p, int B, const
   double x = 0.0, z[3] = {0.0, 0.0, 0.0};
   int flag = bad ? -1 : 0, it = 0, nfact = 0, pol_it = 0, n_ls = 0;
   if (p.method == MPCQP_METHOD_ADMM) flag = admm_qp<N>(p, C, bad, x, z, it, nfact, pol_it, n_ls, dbg);
-  finish_qp<N>(p, b, model, in_x0, in_ref, in_up, C, x, z, flag, it, nfact, pol_it, n_ls, u0o, Xo, Uo, statuso, iterso,
+  finish_qp<N>(p, b, model, in_x0, in_ref, in_up, sm.model, C, x, z, flag, it, nfact, pol_it, n_ls, u0o, Xo, Uo, statuso, iterso,
                activeo);
   if (dbg && threadIdx.x == 0)  // this wave's cycles, start to finish (tools/qp_cycles.py)
     dbg[state_scal_off(N) + 4] = (double)(__builtin_amdgcn_s_memtime() - t_start);

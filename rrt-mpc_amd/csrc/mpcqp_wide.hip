@@ -24,8 +24,8 @@ constexpr int kTW = kT / kWave;
 
 // ---- arena layout (doubles), offsets from the QP's arena base
 struct WideLayout {
-  int N, n, m, ks;  // ks: row stride of K (n + 1: the rows of a column read hit distinct banks)
-  int oK, oModel, oPa, oPg, oE4, oG, oQ, oD, oX, oXt, oRhs, oPx, oAty, oXp, oXa, oDx, oRes, oPd, oXn, oDl, oCol, oCm;
+  int N, n, m, ks, ps;  // ks / ps: row strides of K / Pbar (n + 1: a column's rows hit distinct banks)
+  int oK, oModel, oPa, oPg, oE4, oG, oQ, oD, oX, oXt, oRhs, oPx, oAty, oXp, oXa, oDx, oRes, oPd, oXn, oDl, oCol, oCol2, oCm;
   int oK1, oK2, oEr, oL, oU, oW, oLo0, oHi0, oW0, oZ, oY, oZt, oTmp, oAx, oRw, oZc, oZn, oZd, oEl, oT1, oT2, oCd, oCn,
       oRed, total;
   __host__ __device__ static WideLayout make(int N) {
@@ -34,6 +34,7 @@ struct WideLayout {
     L.n = 2 * N;
     L.m = 5 * N;
     L.ks = L.n + 1;
+    L.ps = L.n + 1;
     int o = 0;
     auto take = [&](int cnt) {
       const int r = o;
@@ -60,7 +61,8 @@ struct WideLayout {
     L.oPd = take(L.n);
     L.oXn = take(L.n);
     L.oDl = take(L.n);
-    L.oCol = take(L.n);
+    L.oCol = take(L.n + 64);  // + padding: the sweep's tail rows read past n
+    L.oCol2 = take(L.n + 64);
     L.oCm = take(L.n);
     L.oK1 = take(2 * L.n);
     L.oK2 = take(3 * L.n);
@@ -92,7 +94,7 @@ struct WideLayout {
 };
 
 // per-QP workspace doubles: Pbar (n x n) + the arena (used when it does not fit in LDS)
-__host__ __device__ inline size_t wide_stride_of(const WideLayout& L) { return (size_t)L.n * L.n + L.total; }
+__host__ __device__ inline size_t wide_stride_of(const WideLayout& L) { return (size_t)L.n * L.ps + L.total; }
 
 // ---- block reductions (maxima: exact, any order; flags)
 struct Blk {
@@ -130,15 +132,116 @@ struct Blk {
 
 __device__ __forceinline__ double lim(double v) { return limit_scaling(v); }
 
+// for (e = tid; e < n * n; e += kT) f(e / n, e % n, e) -- the row/column advanced without a
+// division per element
+template <class F>
+__device__ __forceinline__ void for_ij(int n, int tid, F&& f) {
+  int i = tid / n, j = tid - (tid / n) * n;
+  const int di = kT / n, dj = kT - (kT / n) * n;
+  for (int e = tid; e < n * n; e += kT) {
+    f(i, j, e);
+    i += di;
+    j += dj;
+    if (j >= n) {
+      j -= n;
+      ++i;
+    }
+  }
+}
+
+// In-place symmetric sweep K <- K^{-1} (mpcqp_cpu.c sweep_inverse); false on a bad pivot.
+// Thread (j, part) keeps rows [part*chunk, +chunk) of column j in registers for all n pivots: per
+// pivot the owners of column k publish it (double-buffered, one barrier) and every element is
+// updated exactly as the C code does it -- the same operations, no memory traffic for K.  The
+// tail rows past n and the idle threads run on copies that are never stored or published, so the
+// update is branch-free.  Out of line (its own register allocation, AS: 3 = K in LDS, 1 = in the
+// workspace) -- inlined into the solve it drags the whole kernel into spills.
+template <int CH, int AS>
+__device__ __noinline__ bool sweep_regs(double* Kg, double* c0g, double* c1g, int n, int ks, int tid) {
+#pragma clang fp contract(off)
+  typedef __attribute__((address_space(AS))) double* Ptr;
+  const Ptr Kp = (Ptr)Kg;
+  const Ptr cb0 = (Ptr)c0g, cb1 = (Ptr)c1g;
+  const int per = kT / n;  // threads per column (>= 2: n <= 126)
+  const int j = tid % n, part = tid / n;
+  const int chunk = (n + per - 1) / per;
+  const bool own = part < per;
+  const int i0 = own ? part * chunk : 0;
+  double R[CH];
+#pragma unroll
+  for (int r = 0; r < CH; ++r) R[r] = Kp[(size_t)min(i0 + r, n - 1) * ks + j];
+  for (int k = 0; k < n; ++k) {
+    const Ptr col = (k & 1) ? cb1 : cb0;  // (a two-element array here would live in scratch)
+    if (own && j == k) {
+#pragma unroll
+      for (int r = 0; r < CH; ++r)
+        if (r < chunk && i0 + r < n) col[i0 + r] = R[r];
+    }
+    __syncthreads();
+    const double d = col[k];
+    const double cj = col[j];
+    const Ptr ci = col + i0;  // rows i0 .. i0 + CH - 1 (the buffers are padded past n)
+    constexpr int G = CH < 16 ? CH : 16;  // rows whose column values are in flight at once
+    double cv[G];
+#pragma unroll
+    for (int r = 0; r < G; ++r) cv[r] = ci[r];  // issued before the division they overlap
+    __builtin_amdgcn_sched_barrier(0);
+    if (!(d > 0.0) || !isfinite(d)) return false;  // uniform: every thread reads the same pivot
+    const double inv = 1.0 / d;
+    const double cjk = cj * inv;
+    const bool jk = j == k;
+#pragma unroll
+    for (int g = 0; g < CH; g += G) {
+      if (g) {
+#pragma unroll
+        for (int r = 0; r < G; ++r) cv[r] = ci[g + r];
+        __builtin_amdgcn_sched_barrier(0);
+      }
+#pragma unroll
+      for (int r = 0; r < G; ++r) {  // rows i != k (both arms use the load: no branch per row)
+        const double f = cv[r] * inv;
+        R[g + r] = jk ? f : R[g + r] - f * cj;
+      }
+    }
+    const double rowk = jk ? -inv : cjk;
+    const int rk = k - i0;
+#pragma unroll
+    for (int r = 0; r < CH; ++r) R[r] = r == rk ? rowk : R[r];  // row k: cheap selects
+  }
+  if (own) {
+#pragma unroll
+    for (int r = 0; r < CH; ++r)
+      if (r < chunk && i0 + r < n) Kp[(size_t)(i0 + r) * ks + j] = -R[r];
+  }
+  __syncthreads();
+  return true;
+}
+
 // The per-QP state of the wide solve: pointers into the arena + the workspace Pbar.
 struct Wide {
   WideLayout L;
   double* A;   // arena
+  bool in_lds;  // the arena is in LDS (a compile-time constant of the kernel)
   double* P;   // Pbar, n x n row-major (workspace)
   Blk blk;
   int tid;
   double c;    // cost scaling (uniform)
   double dt;
+#ifdef MPCQP_WIDE_STAMPS  // diagnostic builds: per-phase s_memtime sums of thread 0 -> st[0..15]
+  double* st = nullptr;
+  unsigned long long t_last = 0;
+  __device__ void mark() { if (tid == 0) t_last = __builtin_amdgcn_s_memtime(); }
+  __device__ void stamp(int slot) {
+    if (tid == 0 && st) {
+      const unsigned long long t = __builtin_amdgcn_s_memtime();
+      st[slot] += (double)(t - t_last);
+      t_last = t;
+    }
+  }
+#else
+  __device__ void mark() {}
+  __device__ void stamp(int) {}
+#endif
   __device__ double* at(int off) const { return A + off; }
   __device__ double& K(int i, int j) const { return A[L.oK + i * L.ks + j]; }
 
@@ -187,14 +290,17 @@ struct Wide {
     }
     __syncthreads();
   }
-  // y = M x, M row-major with row stride ms (thread i: the C code's sequential row sum)
+  // y = M x, M row-major with row stride ms (thread i: the C code's sequential row sum; the loads
+  // run ahead of the sum in groups of 8)
   __device__ void matvec(const double* M, int ms, const double* x, double* y) const {
 #pragma clang fp contract(off)
     __syncthreads();
+    const double* __restrict__ xr = x;
     for (int i = tid; i < L.n; i += kT) {
+      const double* __restrict__ row = M + (size_t)i * ms;
       double t = 0.0;
-      const double* row = M + (size_t)i * ms;
-      for (int j = 0; j < L.n; ++j) t += row[j] * x[j];
+#pragma unroll 8
+      for (int j = 0; j < L.n; ++j) t += row[j] * xr[j];
       y[i] = t;
     }
     __syncthreads();
@@ -225,15 +331,14 @@ struct Wide {
         if (ca != 0.0 && cb != 0.0) bd += rw[3 * N + p] * ca * cb;
       }
     }
-    return P[(size_t)i * n + j] + D[i] * D[j] * bd + (i == j ? sig : 0.0);
+    return P[(size_t)i * L.ps + j] + D[i] * D[j] * bd + (i == j ? sig : 0.0);
   }
   __device__ void form(double sig, const double* rw) const {
     const int n = L.n;
     __syncthreads();
-    for (int e = tid; e < n * n; e += kT) {
-      const int i = e / n, j = e - (e / n) * n;
+    for_ij(n, tid, [&](int i, int j, int e) {
       K(i, j) = kkt(i, j, sig, rw);
-    }
+    });
     __syncthreads();
   }
   // y = M x for the Newton matrix M = kkt(., ., 0, rw) (the C code's matvec over its stored M)
@@ -247,37 +352,22 @@ struct Wide {
     }
     __syncthreads();
   }
-  // in-place symmetric sweep K <- K^{-1} (mpcqp_cpu.c sweep_inverse); false on a bad pivot
-  __device__ bool sweep() const {
-#pragma clang fp contract(off)
-    const int n = L.n;
-    double* col = at(L.oCol);
-    for (int k = 0; k < n; ++k) {
-      __syncthreads();
-      const double d = K(k, k);
-      if (!(d > 0.0) || !isfinite(d)) return false;  // uniform: every thread reads the same pivot
-      const double inv = 1.0 / d;
-      for (int i = tid; i < n; i += kT) col[i] = K(i, k);
-      __syncthreads();
-      for (int e = tid; e < n * n; e += kT) {
-        const int i = e / n, j = e - (e / n) * n;
-        if (i == k) {
-          K(k, j) = j == k ? -inv : col[j] * inv;
-        } else if (j == k) {
-          K(i, k) = col[i] * inv;
-        } else {
-          const double f = col[i] * inv;
-          K(i, j) = K(i, j) - f * col[j];
-        }
-      }
+  __device__ __forceinline__ bool sweep() const {
+    const int per = kT / L.n, chunk = (L.n + per - 1) / per;
+    double *Kp = A + L.oK, *c0 = A + L.oCol, *c1 = A + L.oCol2;
+    if (in_lds) {
+      if (chunk <= 16) return sweep_regs<16, 3>(Kp, c0, c1, L.n, L.ks, tid);
+      if (chunk <= 32) return sweep_regs<32, 3>(Kp, c0, c1, L.n, L.ks, tid);
+      return sweep_regs<64, 3>(Kp, c0, c1, L.n, L.ks, tid);
     }
-    __syncthreads();
-    for (int e = tid; e < n * n; e += kT) {
-      const int i = e / n, j = e - (e / n) * n;
-      K(i, j) = -K(i, j);
-    }
-    __syncthreads();
-    return true;
+    if (chunk <= 16) return sweep_regs<16, 1>(Kp, c0, c1, L.n, L.ks, tid);
+    if (chunk <= 32) return sweep_regs<32, 1>(Kp, c0, c1, L.n, L.ks, tid);
+    return sweep_regs<64, 1>(Kp, c0, c1, L.n, L.ks, tid);
+  }
+  // K <- kkt(., ., sig, rw)^{-1} (form_kkt + sweep_inverse of the C code)
+  __device__ __forceinline__ bool form_inverse(double sig, const double* rw) const {
+    form(sig, rw);
+    return sweep();
   }
   __device__ static int code(double z, double l, double u) { return z > u ? 2 : (z < l ? 1 : 0); }
 };
@@ -381,8 +471,8 @@ __device__ bool wide_setup(const mpcqp_params& p, Wide& S) {
         g[2 * (mm - 1)] = hv;
         g[2 * (mm - 1) + 1] = hd;
       } else {
-        S.P[(size_t)(2 * (mm - 1)) * n + col] = hv;
-        S.P[(size_t)(2 * (mm - 1) + 1) * n + col] = hd;
+        S.P[(size_t)(2 * (mm - 1)) * L.ps + col] = hv;
+        S.P[(size_t)(2 * (mm - 1) + 1) * L.ps + col] = hd;
       }
     }
     const double r00 = R[0][0] / (dt * dt), r10 = R[1][0] / dt;
@@ -391,15 +481,15 @@ __device__ bool wide_setup(const mpcqp_params& p, Wide& S) {
       g[0] += -x0[3] * r00;
       g[1] += -x0[3] * r10;
     } else if (cc == 0) {
-      H[(size_t)col * n + col] += j + 1 < N ? 2.0 * r00 : r00;
-      if (j >= 1) H[(size_t)(col - 2) * n + col] += -r00;
-      if (j + 1 < N) H[(size_t)(col + 2) * n + col] += -r00;
-      H[(size_t)(col + 1) * n + col] += r10;
-      if (j + 1 < N) H[(size_t)(col + 3) * n + col] += -r10;
+      H[(size_t)col * L.ps + col] += j + 1 < N ? 2.0 * r00 : r00;
+      if (j >= 1) H[(size_t)(col - 2) * L.ps + col] += -r00;
+      if (j + 1 < N) H[(size_t)(col + 2) * L.ps + col] += -r00;
+      H[(size_t)(col + 1) * L.ps + col] += r10;
+      if (j + 1 < N) H[(size_t)(col + 3) * L.ps + col] += -r10;
     } else {
-      H[(size_t)(col - 1) * n + col] += r10;
-      if (j >= 1) H[(size_t)(col - 3) * n + col] += -r10;
-      H[(size_t)col * n + col] += R[1][1];
+      H[(size_t)(col - 1) * L.ps + col] += r10;
+      if (j >= 1) H[(size_t)(col - 3) * L.ps + col] += -r10;
+      H[(size_t)col * L.ps + col] += R[1][1];
     }
   }
   __syncthreads();
@@ -411,7 +501,7 @@ __device__ bool wide_setup(const mpcqp_params& p, Wide& S) {
   double* lo0 = S.at(L.oLo0);
   double* hi0 = S.at(L.oHi0);
   double* w0 = S.at(L.oW0);
-  for (int e = tid; e < n * n; e += kT) S.P[e] = 2.0 * S.P[e];
+  for_ij(n, tid, [&](int i, int j, int) { S.P[(size_t)i * L.ps + j] = 2.0 * S.P[(size_t)i * L.ps + j]; });
   const double idt = 1.0 / p.dt, v0 = x0[3];
   for (int i = tid; i < n; i += kT) {
     q[i] = 2.0 * g[i];
@@ -453,7 +543,8 @@ __device__ bool wide_setup(const mpcqp_params& p, Wide& S) {
   for (int it = 0; it < p.scaling; ++it) {
     for (int qq = tid; qq < n; qq += kT) {
       double cp = 0.0;
-      for (int i = 0; i < n; ++i) cp = fmax(cp, fabs(S.P[(size_t)i * n + qq]));
+#pragma unroll 8
+      for (int i = 0; i < n; ++i) cp = fmax(cp, fabs(S.P[(size_t)i * L.ps + qq]));
       cp *= cpend;
       double cc = (qq & 1) == 0 ? E[qq / 2] : 0.0;
       cc = fmax(cc, E[N + qq] * fabs(k1[2 * qq]));
@@ -473,11 +564,10 @@ __device__ bool wide_setup(const mpcqp_params& p, Wide& S) {
     }
     for (int j = tid; j < N; j += kT) el[j] = 1.0 / sqrt(lim(E[j] * D[2 * j]));
     __syncthreads();
-    for (int e = tid; e < n * n; e += kT) {
-      const int i = e / n, j = e - (e / n) * n;
+    for_ij(n, tid, [&](int i, int j, int e) {
       const double dlc = dl[j] * cpend;
-      S.P[e] = S.P[e] * (dl[i] * dlc);
-    }
+      S.P[(size_t)i * L.ps + j] = S.P[(size_t)i * L.ps + j] * (dl[i] * dlc);
+    });
     for (int i = tid; i < n; i += kT) {
       D[i] *= dl[i];
       q[i] *= dl[i];
@@ -487,12 +577,14 @@ __device__ bool wide_setup(const mpcqp_params& p, Wide& S) {
     double qm = 0.0;
     for (int qq = tid; qq < n; qq += kT) {
       double cp = 0.0;
-      for (int i = 0; i < n; ++i) cp = fmax(cp, fabs(S.P[(size_t)i * n + qq]));
+#pragma unroll 8
+      for (int i = 0; i < n; ++i) cp = fmax(cp, fabs(S.P[(size_t)i * L.ps + qq]));
       cm[qq] = cp;
       qm = fmax(qm, fabs(q[qq]));
     }
     qm = S.blk.max(qm);  // synchronizes: cm complete
     double cn = 0.0;
+#pragma unroll 8
     for (int qq = 0; qq < n; ++qq) cn += cm[qq];  // every thread, the C code's order
     cn /= n;
     const double ct = 1.0 / lim(fmax(cn, lim(qm)));
@@ -501,7 +593,7 @@ __device__ bool wide_setup(const mpcqp_params& p, Wide& S) {
     c *= ct;
     __syncthreads();
   }
-  for (int e = tid; e < n * n; e += kT) S.P[e] *= cpend;
+  for_ij(n, tid, [&](int i, int j, int) { S.P[(size_t)i * L.ps + j] *= cpend; });
   double* l = S.at(L.oL);
   double* u = S.at(L.oU);
   double* w = S.at(L.oW);
@@ -514,7 +606,7 @@ __device__ bool wide_setup(const mpcqp_params& p, Wide& S) {
   __syncthreads();
   bool bad = false;
   for (int i = tid; i < n; i += kT) bad = bad || !isfinite(q[i]);
-  for (int e = tid; e < n * n; e += kT) bad = bad || !isfinite(S.P[e]);
+  for_ij(n, tid, [&](int i, int j, int) { bad = bad || !isfinite(S.P[(size_t)i * L.ps + j]); });
   for (int rr = tid; rr < m; rr += kT) bad = bad || !isfinite(l[rr]) || !isfinite(u[rr]);
   return S.blk.any(bad);
 }
@@ -544,7 +636,7 @@ __device__ int wide_polish(Wide& S, double* x, const double* zg, int max_it, int
   double* t1 = S.at(L.oT1);
   double* t2 = S.at(L.oT2);
   S.Cmul(x, zc);
-  S.matvec(S.P, n, x, Px);
+  S.matvec(S.P, L.ps, x, Px);
   for (int r = tid; r < m; r += kT) cd[r] = Wide::code(zg[r], l[r], u[r]);
   __syncthreads();
   for (int it = 1; it <= max_it; ++it) {
@@ -553,9 +645,10 @@ __device__ int wide_polish(Wide& S, double* x, const double* zg, int max_it, int
       rw[r] = cd[r] != 0.0 ? 2.0 * w[r] : 0.0;
       tmp[r] = cd[r] == 2.0 ? rw[r] * u[r] : (cd[r] == 1.0 ? rw[r] * l[r] : 0.0);
     }
-    S.form(0.0, rw);
+    S.mark();
     ++n_fact;
-    if (!S.sweep()) return -1;
+    if (!S.form_inverse(0.0, rw)) return -1;
+    S.stamp(5);
     S.CTmul(tmp, rhs);
     for (int i = tid; i < n; i += kT) rhs[i] -= q[i];
     S.matvec(&S.K(0, 0), L.ks, rhs, xn);
@@ -564,6 +657,7 @@ __device__ int wide_polish(Wide& S, double* x, const double* zg, int max_it, int
     for (int i = tid; i < n; i += kT) nf = nf || !isfinite(xn[i]);
     for (int r = tid; r < m; r += kT) diff = diff || Wide::code(zn[r], l[r], u[r]) != cd[r];
     if (S.blk.any(nf)) return -1;
+    S.stamp(6);
     if (!S.blk.any(diff)) {
       // the set reproduces itself: one step of iterative refinement, then accept if it still does
       S.kkt_matvec(rw, xn, res);
@@ -593,6 +687,7 @@ __device__ int wide_polish(Wide& S, double* x, const double* zg, int max_it, int
     for (int r = tid; r < m; r += kT) zd[r] = zn[r] - zc[r];
     __syncthreads();
     double qd = 0.0, lin = 0.0;  // every thread, the C code's order
+#pragma unroll 8
     for (int i = 0; i < n; ++i) {
       qd += dx[i] * Pd[i];
       lin += (Px[i] + q[i]) * dx[i];
@@ -608,6 +703,7 @@ __device__ int wide_polish(Wide& S, double* x, const double* zg, int max_it, int
       }
       __syncthreads();
       double d1 = lin + t * qd, d2 = qd;
+#pragma unroll 8
       for (int r = 0; r < m; ++r) {  // the C code's order; d2 takes the rows with rr != 0 only
         d1 += t1[r];
         if (t2[r] >= 0.0) d2 += t2[r];
@@ -631,6 +727,7 @@ __device__ int wide_polish(Wide& S, double* x, const double* zg, int max_it, int
     S.Cmul(x, zc);
     for (int r = tid; r < m; r += kT) cd[r] = Wide::code(zc[r], l[r], u[r]);
     __syncthreads();
+    S.stamp(7);
   }
   return 0;
 }
@@ -672,15 +769,16 @@ __device__ void wide_solve(const mpcqp_params& p, Wide& S, bool bad, int b, doub
     const double sig = p.sigma, a = p.alpha;
     bool refactor = true;
     for (int it = 1; it <= p.max_iter && !bad; ++it) {
+      S.mark();
       if (refactor) {
         for (int r = tid; r < m; r += kT) rw[r] = rho;
-        S.form(sig, rw);
         ++n_fact;
-        if (!S.sweep()) {
+        if (!S.form_inverse(sig, rw)) {
           bad = true;
           break;
         }
         refactor = false;
+        S.stamp(1);
       }
       for (int r = tid; r < m; r += kT) tmp[r] = rho * z[r] - y[r];
       S.CTmul(tmp, rhs);
@@ -701,10 +799,11 @@ __device__ void wide_solve(const mpcqp_params& p, Wide& S, bool bad, int b, doub
         z[r] = zn;
       }
       __syncthreads();
+      S.stamp(2);
       admm_it = it;
       if (it % p.check_termination == 0 || it == p.max_iter) {
         S.Cmul(x, Ax);
-        S.matvec(S.P, n, x, Px);
+        S.matvec(S.P, L.ps, x, Px);
         S.CTmul(y, Aty);
         double pr = 0, nAx = 0, nz = 0, spr = 0, snAx = 0, snz = 0;
         double du = 0, nPx = 0, nAty = 0, nq = 0, sdu = 0, snPx = 0, snAty = 0, snq = 0;
@@ -747,6 +846,7 @@ __device__ void wide_solve(const mpcqp_params& p, Wide& S, bool bad, int b, doub
         snAty = S.blk.max(snAty);
         snq = S.blk.max(snq);
         nonfinite = S.blk.any(nonfinite);
+        S.stamp(3);
         const double ic = 1.0 / S.c;
         du *= ic;
         const double ep = p.eps_abs + p.eps_rel * fmax(nAx, nz);
@@ -892,9 +992,14 @@ __device__ void wide_solve(const mpcqp_params& p, Wide& S, bool bad, int b, doub
   }
 }
 
+// kMode: where the arena and Pbar live -- 2 both in LDS, 1 the arena in LDS and Pbar in the
+// workspace, 0 both in the workspace.  A compile-time choice, so every access is a ds_* or a
+// global_* instruction (a pointer that may be either compiles to flat accesses, which wait for
+// all outstanding memory operations: ~100x slower here).
+template <int kMode>
 __global__ __launch_bounds__(kT) void k_solve_wide(mpcqp_params p, int B, const uint8_t* __restrict__ mask,
                                                    const double* __restrict__ model, double* __restrict__ wide,
-                                                   int arena_lds, double* __restrict__ u0o, double* __restrict__ Xo,
+                                                   double* __restrict__ u0o, double* __restrict__ Xo,
                                                    double* __restrict__ Uo, int32_t* __restrict__ statuso,
                                                    int32_t* __restrict__ iterso, uint8_t* __restrict__ activeo) {
   extern __shared__ double lds[];
@@ -907,13 +1012,31 @@ __global__ __launch_bounds__(kT) void k_solve_wide(mpcqp_params p, int B, const 
   S.dt = p.dt;
   S.c = 1.0;
   double* qp = wide + (size_t)b * wide_stride_of(S.L);
-  S.P = qp;
-  S.A = arena_lds ? lds : qp + (size_t)n * n;
+  S.in_lds = kMode != 0;
+  if constexpr (kMode == 2) {
+    S.A = lds;
+    S.P = lds + S.L.total;
+  } else if constexpr (kMode == 1) {
+    S.A = lds;
+    S.P = qp;
+  } else {
+    S.A = qp + (size_t)n * S.L.ps;
+    S.P = qp;
+  }
   S.blk.red = S.A + S.L.oRed;
   const double* mb = model + (size_t)b * model_stride(N);
   for (int i = S.tid; i < model_stride(N); i += kT) S.A[S.L.oModel + i] = mb[i];
   __syncthreads();
+#ifdef MPCQP_WIDE_STAMPS
+  if constexpr (kMode != 0) {
+    S.st = qp + (size_t)n * S.L.ps;
+    if (S.tid < 16) S.st[S.tid] = 0.0;
+    __syncthreads();
+  }
+#endif
+  S.mark();
   const bool bad = wide_setup(p, S);
+  S.stamp(0);
   wide_solve(p, S, bad, b, u0o, Xo, Uo, statuso, iterso, activeo);
 }
 
@@ -922,18 +1045,23 @@ __global__ __launch_bounds__(kT) void k_solve_wide(mpcqp_params p, int B, const 
 namespace mpcqp {
 size_t wide_stride(int horizon) { return wide_stride_of(WideLayout::make(horizon)); }
 
-// LDS bytes of the arena when it is placed on chip, 0 when it goes to the workspace
-static size_t wide_lds_bytes(int horizon) {
-  const size_t bytes = sizeof(double) * (size_t)WideLayout::make(horizon).total;
-  return bytes <= 160u * 1024u ? bytes : 0;
-}
-
 void launch_solve_wide(hipStream_t s, const Launch& L) {
   double* wide = L.state;
-  const size_t lds = wide_lds_bytes(L.p->horizon);
-  if (lds > 65536) (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_solve_wide),
-                                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-  hipLaunchKernelGGL(k_solve_wide, dim3(L.B), dim3(kT), lds, s, *L.p, L.B, L.mask, L.model, wide, lds > 0 ? 1 : 0,
-                     L.u0, L.X, L.U, L.st, L.it, L.ac);
+  const WideLayout lay = WideLayout::make(L.p->horizon);
+  const size_t arena = sizeof(double) * (size_t)lay.total, pbar = sizeof(double) * (size_t)lay.n * lay.ps;
+  constexpr size_t kLds = 160u * 1024u;
+  auto go = [&](auto kern, size_t lds) {
+    if (lds > 65536)
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)lds);
+    hipLaunchKernelGGL(kern, dim3(L.B), dim3(kT), lds, s, *L.p, L.B, L.mask, L.model, wide, L.u0, L.X, L.U, L.st,
+                       L.it, L.ac);
+  };
+  if (arena + pbar <= kLds)
+    go(&k_solve_wide<2>, arena + pbar);
+  else if (arena <= kLds)
+    go(&k_solve_wide<1>, arena);
+  else
+    go(&k_solve_wide<0>, 0);
 }
 }  // namespace mpcqp

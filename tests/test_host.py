@@ -268,5 +268,8 @@ def test_solver_kernel_resources():
     res = {int(k): v for k, v in json.loads(path.read_text()).items()}
     assert sorted(res) == list(range(1, 32))
     for N, r in res.items():
-        assert r["Occupancy"] >= 2 and r["AGPRs"] == 0, (N, r)
-        assert r["ScratchSize"] <= (0 if N <= 28 else 64), (N, r)
+        # N >= 29: Pbar's LDS already caps a CU at 5 workgroups; the kernel takes one wave's
+        # register file per SIMD (a few AGPRs as spill space) instead of scratch memory
+        assert r["Occupancy"] >= (2 if N <= 28 else 1), (N, r)
+        assert r["AGPRs"] == 0 or N >= 29, (N, r)
+        assert r["ScratchSize"] == 0, (N, r)

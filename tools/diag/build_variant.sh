@@ -5,5 +5,5 @@
 set -e
 cd "$(dirname "$0")/../.."
 name=$1; shift
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared -Wno-unused-result -DMPCQP_ONLY_N=20 "$@" \
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared -Wno-unused-result -DMPCQP_ONLY_N=${ONLY_N:-20} "$@" \
   -o tools/diag/libmpcqp_$name.so rrt-mpc_amd/csrc/mpcqp.hip rrt-mpc_amd/csrc/mpcqp_fleet.hip rrt-mpc_amd/csrc/mpcqp_refbuild.hip rrt-mpc_amd/csrc/mpcqp_rrt.hip rrt-mpc_amd/csrc/mpcqp_inflate.hip rrt-mpc_amd/csrc/mpcqp_wide.hip rrt-mpc_amd/csrc/mpcqp_swarm.hip
