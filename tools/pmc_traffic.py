@@ -23,11 +23,13 @@ from pathlib import Path
 SOLVE = ("k_solve",)
 
 
-def per_kernel(path: Path) -> dict:
+def per_kernel(path: Path, N: int) -> dict:
+    """Mean counter value per (kernel, counter); k_solve = k_solve<N> only (bench.py also runs the
+    config-1 loop's B=1 k_solve<10> launches, which must not dilute the averages)."""
     acc = collections.defaultdict(list)
     for r in csv.DictReader(open(path)):
         name = r["Kernel_Name"]
-        short = next((k for k in (*SOLVE, "k_build") if k in name), None)
+        short = "k_solve" if f"k_solve<{N}>" in name else ("k_build" if "k_build" in name else None)
         if short:
             acc[(short, r["Counter_Name"])].append(float(r["Counter_Value"]))
     return {k: sum(v) / len(v) for k, v in acc.items()}
@@ -44,13 +46,15 @@ def main() -> None:
     for p in ("pmc_fetch", "pmc_write", "pmc_req", "pmc_sq", "pmc_f64"):
         f = d / p / "run_counter_collection.csv"
         if f.exists():
-            c.update(per_kernel(f))
+            c.update(per_kernel(f, a.N))
     kib = 1024.0
-    fetch = {k: c[(k, "FETCH_SIZE")] * kib for k in (*SOLVE, "k_build")}
-    write = {k: c[(k, "WRITE_SIZE")] * kib for k in (*SOLVE, "k_build")}
-    rdreq = {k: c.get((k, "TCC_EA0_RDREQ_sum")) for k in (*SOLVE, "k_build")}
+    kernels = [k for k in (*SOLVE, "k_build") if (k, "FETCH_SIZE") in c]  # k_build: absent when K1 is fused
+    fetch = {k: c[(k, "FETCH_SIZE")] * kib for k in kernels}
+    write = {k: c[(k, "WRITE_SIZE")] * kib for k in kernels}
+    rdreq = {k: c.get((k, "TCC_EA0_RDREQ_sum")) for k in kernels}
     N, B = a.N, a.B
-    build_read_alg = 8.0 * B * (4 * (N + 1) + 6)
+    build_read_alg = 8.0 * B * (4 * (N + 1) + 6)  # K1's inputs: x0, ref window, u_prev
+    out_alg = 8.0 * B * (2 + 4 * (N + 1) + 2 * N) + B * (4 + 16 + 5 * N + 1)  # u0, X, U, status, iters, active
     read = 2.0 * sum(fetch[k] for k in SOLVE)
     wr = sum(write[k] for k in SOLVE)
     out = {
@@ -61,13 +65,14 @@ def main() -> None:
             "per_kernel_fetch_bytes_raw": fetch,
             "per_kernel_write_bytes": write,
             "per_kernel_tcc_ea0_rdreq": rdreq,
-            "k_build_read_calibration": {"algorithmic_read_bytes": build_read_alg,
-                                          "fetch_bytes_raw": fetch["k_build"],
-                                          "ratio": build_read_alg / fetch["k_build"]},
+            "algorithmic_bytes_per_launch": {"read": build_read_alg, "write": out_alg,
+                                             "total": build_read_alg + out_alg},
+            "hbm_over_algorithmic": (read + wr) / (build_read_alg + out_alg),
             "per_qp_bytes": (read + wr) / B,
-            "note": "FETCH doubled per the gfx950 correction (8-byte-per-lane loads: an upper bound, "
-                    "k_build calibrates that width); k_solve reads the 1.8 KB model per QP and "
-                    "writes the outputs; the scaled problem stays on chip",
+            "note": "FETCH doubled per the gfx950 correction (8-byte-per-lane loads: an upper bound); "
+                    + ("K1 separate: k_solve reads the model block per QP; " if "k_build" in fetch else
+                       "K1 fused: k_solve reads the inputs (x0, ref window, u_prev) itself; ")
+                    + "it writes the outputs; the scaled problem stays on chip",
         }
     }
     sq = {name: v for (k, name), v in c.items() if k == "k_solve" and name.startswith("SQ_")}
