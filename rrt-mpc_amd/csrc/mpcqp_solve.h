@@ -11,8 +11,32 @@ using mpcqp::Launch;
 #ifndef MPCQP_MODEL_KEEP  // development switch (A/B builds): 0 never keeps the model in LDS
 #define MPCQP_MODEL_KEEP 1
 #endif
+// Development switches (A/B builds).  MPCQP_BCAST_LDS 1 stages the dense products' broadcasts
+// through LDS (no VALU work) instead of permlane swaps: measured slower (B=4096 +3 %, B=512 +9 %:
+// the LDS round trip is on every product's critical path).  MPCQP_PIVOT_SGPR 1 reads the sweep's
+// pivot by readlane (off the broadcast's critical path) instead of from the broadcast copy.
+#ifndef MPCQP_BCAST_LDS
+#define MPCQP_BCAST_LDS 0
+#endif
+#ifndef MPCQP_PIVOT_SGPR
+#define MPCQP_PIVOT_SGPR 1
+#endif
+#ifndef MPCQP_BCAST_LDS_SWEEP  // ... for the sweep's pivot columns
+#define MPCQP_BCAST_LDS_SWEEP MPCQP_BCAST_LDS
+#endif
 template <int N>
-constexpr bool kModelKept = MPCQP_MODEL_KEEP && 32 * N * N + 8 * model_stride(N) <= 163840 / 8;
+struct SolveSmem {
+  static constexpr int n = 2 * N;
+  static constexpr int kPS = n + 1;  // row stride: column n is a zero padding column
+  double pad0[4];     // zeros: form()'s band writes of the first rows land here when out of range
+  double P[n * kPS];  // Pbar, row-major (lane `col` reads column col: conflict-free; lanes >= n read the zeros of column n)
+  double pad1[4];     // zeros: ... and those of the last rows
+  double band[5][n];  // Pbar's entries at form()'s band addresses (lane p: (p, p + 2d - 4)), restored after each form
+};
+
+template <int N>
+constexpr bool kModelKept =
+    MPCQP_MODEL_KEEP && 8 * (int)sizeof(SolveSmem<N>) + 8 * 8 * kWave + 64 * model_stride(N) <= 163840;
 
 template <int N>
 struct SetupSmem {
@@ -25,16 +49,12 @@ struct SetupSmem {
 };
 
 template <int N>
-struct SolveSmem {
-  double P[4 * N * N];  // Pbar, row-major n x n (lane `col` reads column col: conflict-free)
-};
-
-template <int N>
 struct SolveLds {
   union {
     SetupSmem<N> setup;
     SolveSmem<N> solve;  // setup_qp writes Pbar when its own LDS data is dead
   };
+  double bc[kWave];  // broadcast staging of the dense row-per-lane products (Ctx::vbcast)
   double model[kModelKept<N> ? model_stride(N) : 1];  // the model block, live to the end (kModelKept)
   __device__ double* model_ptr() { return kModelKept<N> ? model : setup.model; }
 };
@@ -44,10 +64,11 @@ struct SolveLds {
 // Variables W = (v_1, delta_0, v_2, delta_1, ...): lane 2j holds the speed v_{j+1}, lane 2j+1
 // the steering delta_j.  The rows owned by lane p (slot 0: v row, p even; slot 1: input row;
 // slot 2: rate row) are banded in those variables:
-//   slot 0  v_{p/2+1}                                    (identity)
-//   slot 1  e1[0] t_p + e1[1] t_{p-2}                    (a_j = (v_{j+1} - v_j)/dt; delta_j)
-//   slot 2  e2[0] t_p + e2[1] t_{p-2} + e2[2] t_{p-4}    (a_j - a_{j-1}; delta_j - delta_{j-1})
-// with t = D x and e the row coefficients times the row scaling E.
+//   slot 0  c0 x_p                                      (v_{p/2+1}: identity)
+//   slot 1  c10 x_p + c11 x_{p-2}                       (a_j = (v_{j+1} - v_j)/dt; delta_j)
+//   slot 2  c20 x_p + c21 x_{p-2} + c22 x_{p-4}         (a_j - a_{j-1}; delta_j - delta_{j-1})
+// with c = (row scaling E x row coefficient) x the column scaling D of the variable it multiplies:
+// the scaled operator Cbar = E C D with D folded into the coefficients.
 template <int N>
 struct Ctx {
   static constexpr int n = 2 * N;
@@ -56,17 +77,26 @@ struct Ctx {
   double dt;
   double D, qv;
   double E[3], lo[3], hi[3], wb[3];
-  double e1[2], e2[3];
+  double c0, c10, c11, c20, c21, c22;  // Cbar's coefficients (see above)
   double cscale;
-  const double* __restrict__ P;  // Pbar (LDS, row-major n x n)
+  static constexpr int kPS = SolveSmem<N>::kPS;  // Pbar row stride
+  double* __restrict__ P;  // Pbar (LDS, row-major n x n, row stride kPS)
+  double* __restrict__ bc;  // LDS broadcast staging (kWave doubles)
+  const double* __restrict__ band;  // SolveSmem::band
   static constexpr int kNW = (n + 15) / 16;  // 16-lane rows holding the n variables
   // KKT inverse, row `lane`: A^{-1}[lane][j] = -r[j] (symmetric sweep operator)
   double r[n];
+  // work counters (written to the solver state with debug_state; tools/qp_cycles.py)
+  int n_full, n_r1;
 
   // Bind the context to this lane and the solve LDS (Pbar); the problem data fields are
   // filled by setup_qp.
-  __device__ __forceinline__ void init(int ln, double dt_, SolveSmem<N>& s) {
+  __device__ __forceinline__ void init(int ln, double dt_, SolveSmem<N>& s, double* bcast_buf) {
     lane = ln;
+    bc = bcast_buf;
+    band = &s.band[0][0];
+    n_full = 0;
+    n_r1 = 0;
     act = ln < n;
     even = act && ((ln & 1) == 0);
     dt = dt_;
@@ -79,29 +109,57 @@ struct Ctx {
   __device__ __forceinline__ void opaque() {
     asm volatile("" : "+v"(D), "+v"(qv), "+v"(lane));
     asm volatile("" : "+v"(E[0]), "+v"(E[1]), "+v"(E[2]));
-    asm volatile("" : "+v"(e1[0]), "+v"(e1[1]), "+v"(e2[0]), "+v"(e2[1]), "+v"(e2[2]));
+    asm volatile("" : "+v"(c0), "+v"(c10), "+v"(c11), "+v"(c20), "+v"(c21), "+v"(c22));
     asm volatile("" : "+v"(lo[0]), "+v"(lo[1]), "+v"(lo[2]));
     asm volatile("" : "+v"(hi[0]), "+v"(hi[1]), "+v"(hi[2]));
     asm volatile("" : "+v"(wb[0]), "+v"(wb[1]), "+v"(wb[2]));
   }
 
+  // Every lane's view of v (one element per lane): w[c] lane l = v[16 c + (l & 15)], read by the
+  // fmac_bc products through DPP row_newbcast.  Default: bcast() (permlane16/32 swaps + copies,
+  // ~12 VALU instructions, ~110 cycles).  LDS staging (one ds_write + kNW ds_reads, no VALU work;
+  // one wave per workgroup executes its LDS operations in order, so only compiler ordering points
+  // are needed) measured slower: its round trip is on every product's critical path.
+  template <bool LDS = MPCQP_BCAST_LDS>
+  __device__ __forceinline__ void vbcast(double v, double w[4]) const {
+    if constexpr (LDS) {
+    lds_sync();
+    bc[lane] = v;
+    lds_sync();
+    const double* b = bc + (lane & 15);
+    Unroll<0, kNW>::run([&](auto cc) {
+      constexpr int c = decltype(cc)::value;
+      w[c] = b[16 * c];
+    });
+    } else {
+      bcast<kNW>(v, w);
+    }
+  }
+  // element j of the vector last staged by vbcast<LDS>, in every lane
+  template <int J, bool LDS = MPCQP_BCAST_LDS>
+  __device__ __forceinline__ double staged(const double w[4]) const {
+    if constexpr (LDS) {
+      (void)w;
+      return bc[J];
+    } else {
+      return dpp<0x150 + (J % 16)>(w[J / 16]);
+    }
+  }
+
   // z = Cbar x: shifts only (no scans)
   __device__ __forceinline__ void Cmul(double x, double z[3]) const {
-    const double t = D * x;
-    const double tm2 = shr2(t);
-    const double tm4 = shr2(tm2);
-    z[0] = E[0] * t;
-    z[1] = e1[0] * t + e1[1] * tm2;
-    z[2] = (e2[0] * t + e2[1] * tm2) + e2[2] * tm4;
+    const double xm2 = shr2(x);
+    const double xm4 = shr2(xm2);
+    z[0] = c0 * x;
+    z[1] = c10 * x + c11 * xm2;
+    z[2] = (c20 * x + c21 * xm2) + c22 * xm4;
   }
-  // x = Cbar' y
+  // x = Cbar' y: the terms for the variables 2 and 4 back shifted in one chain, shl2(a + shl2(b))
   __device__ __forceinline__ double CTmul(const double y[3]) const {
-    const double a = e1[1] * y[1] + e2[1] * y[2];  // to the variable 2 back
-    const double b = e2[2] * y[2];                 // to the variable 4 back
-    double t = (E[0] * y[0] + e1[0] * y[1]) + e2[0] * y[2];
-    t += shl2(a);
-    t += shl4(b);
-    return D * t;
+    const double a = c11 * y[1] + c21 * y[2];  // to the variable 2 back
+    const double b = c22 * y[2];               // to the variable 4 back
+    const double t = (c0 * y[0] + c10 * y[1]) + c20 * y[2];
+    return t + shl2(a + shl2(b));
   }
   // (Pbar v)_lane, Pbar symmetric: lane reads its row as a conflict-free column of the LDS copy
   // The column loads go out in groups of kPG ahead of their FMAs (the inline-asm FMAs pin each
@@ -110,27 +168,27 @@ struct Ctx {
   static constexpr int kPG = 4;
   __device__ __forceinline__ double Pmul(double v) const {
     double w[4];
-    bcast<kNW>(act ? v : 0.0, w);
-    const int col = act ? lane : 0;
+    vbcast(act ? v : 0.0, w);
+    const int col = act ? lane : n;  // lanes >= n read the zero padding column
     double a[4] = {0.0, 0.0, 0.0, 0.0};
     if constexpr (N > 24) {
       Unroll<0, n>::run([&](auto jc) {
         constexpr int j = decltype(jc)::value;
-        fmac_bc<j % 16>(a[j % 4], w[j / 16], P[j * n + col]);
+        fmac_bc<j % 16>(a[j % 4], w[j / 16], P[j * kPS + col]);
       });
       return act ? (a[0] + a[1]) + (a[2] + a[3]) : 0.0;
     }
     double cur[kPG], nxt[kPG];
     Unroll<0, kPG>::run([&](auto kc) {
       constexpr int k = decltype(kc)::value;
-      cur[k] = k < n ? P[k * n + col] : 0.0;
+      cur[k] = k < n ? P[k * kPS + col] : 0.0;
     });
     Unroll<0, (n + kPG - 1) / kPG>::run([&](auto gc) {
       constexpr int g = decltype(gc)::value;
       if constexpr ((g + 1) * kPG < n) {
         Unroll<0, kPG>::run([&](auto kc) {
           constexpr int j = (g + 1) * kPG + decltype(kc)::value;
-          nxt[decltype(kc)::value] = j < n ? P[j * n + col] : 0.0;
+          nxt[decltype(kc)::value] = j < n ? P[j * kPS + col] : 0.0;
         });
       }
       __builtin_amdgcn_sched_barrier(0);  // the next group's loads stay ahead of this group's FMAs
@@ -144,32 +202,76 @@ struct Ctx {
   }
   // KKT matrix A = Pbar + s I + Cbar' diag(rw) Cbar, row `lane` -> r[].  The row part is a
   // band (lanes p-4 .. p+4 of the same kind): its five entries per lane come from shifts.
+  // From n >= 8 on, each lane adds its five band entries into its own row of Pbar in LDS
+  // (read-modify-write), every lane loads its row as a column of the sum, and the lanes write the
+  // original entries back: ~10 VALU instructions instead of a compare-and-select per column (the
+  // band position j = lane + d is lane dependent, so registers cannot be addressed by it).
+  // Entries outside the matrix have band value +-0: their addresses land in the zero padding
+  // column, in pad0 / pad1, or (n >= 8) on an entry of a neighbouring row that no lane's band
+  // touches, which gets its own value back.
   __device__ __forceinline__ void form(double s, const double rw[3]) {
     // opaque lane copy: keeps per-column masks/addresses from being hoisted out of solver loops
     int ln = lane;
     asm volatile("" : "+v"(ln));
-    const double a1 = rw[1] * e1[1], a2 = rw[2] * e2[1], b2 = rw[2] * e2[2];
-    const double dg = (E[0] * E[0] * rw[0] + rw[1] * e1[0] * e1[0]) + rw[2] * e2[0] * e2[0];
-    const double diag = dg + shl2(a1 * e1[1] + a2 * e2[1]) + shl4(b2 * e2[2]);
-    const double up2 = shl2(a1 * e1[0] + a2 * e2[0]) + shl4(b2 * e2[1]);  // entry (p, p+2)
-    const double up4 = shl4(b2 * e2[0]);                                  // entry (p, p+4)
-    const double b0 = D * D * diag + s;
-    const double bp2 = D * shl2(D) * up2, bp4 = D * shl4(D) * up4;
+    // row r of lane q (weight rw) adds rw c_i c_j at (q - 2i, q - 2j): lane p's diagonal takes its
+    // own rows' c_0 terms, lane p+2's c_1 terms and lane p+4's c_2 terms, and so on
+    const double a1 = rw[1] * c11, a2 = rw[2] * c21, b2 = rw[2] * c22;
+    const double dg = (c0 * c0 * rw[0] + rw[1] * c10 * c10) + rw[2] * c20 * c20;
+    const double b0 = (dg + shl2(a1 * c11 + a2 * c21) + shl4(b2 * c22)) + s;
+    const double bp2 = shl2(a1 * c10 + a2 * c20) + shl4(b2 * c21);  // entry (p, p+2)
+    const double bp4 = shl4(b2 * c20);                               // entry (p, p+4)
     const double bm2 = shr2(bp2), bm4 = shr4(bp4);  // symmetric: (p, p-2) = lane p-2's (., +2)
-    const int col = ln < n ? ln : 0;
     const bool live = ln < n;
-    // every lane loads (lanes >= n read column 0 and discard it): no exec-masked load per column
-    Unroll<0, n>::run([&](auto jc) {
-      constexpr int j = decltype(jc)::value;
-      double t = 0.0;
-      if (j == ln) t = b0;
-      if (j == ln + 2) t = bp2;
-      if (j + 2 == ln) t = bm2;
-      if (j == ln + 4) t = bp4;
-      if (j + 4 == ln) t = bm4;
-      const double pv = P[j * n + col];
-      r[j] = live ? pv + t : 0.0;
-    });
+    if constexpr (n >= 8) {
+      // entry (ln, ln - 4) (positive immediate offsets) and the saved originals, saved by setup_qp
+      double* rowp = P + ln * (kPS + 1) - 4;
+      const double* bo = band + ln;
+      lds_sync();
+      if (live) {
+        rowp[0] = bo[0 * n] + bm4;
+        rowp[2] = bo[1 * n] + bm2;
+        rowp[4] = bo[2 * n] + b0;
+        rowp[6] = bo[3 * n] + bp2;
+        rowp[8] = bo[4 * n] + bp4;
+      }
+      lds_sync();
+      // lanes >= n: the zero padding column, so their rows are exactly zero (from the opaque lane
+      // copy: the column addresses are recomputed per form, not hoisted into live registers)
+      const int c = live ? ln : n;
+      Unroll<0, n>::run([&](auto jc) {
+        constexpr int j = decltype(jc)::value;
+        r[j] = P[j * kPS + c];
+      });
+      lds_sync();
+      // restore Pbar; the addresses are recomputed from an opaque lane copy, so nothing but r[]
+      // stays live across the loads
+      int l2 = lane;
+      asm volatile("" : "+v"(l2));
+      if (l2 < n) {
+        double* rp = P + l2 * (kPS + 1) - 4;
+        const double* bp = band + l2;
+        rp[0] = bp[0 * n];
+        rp[2] = bp[1 * n];
+        rp[4] = bp[2 * n];
+        rp[6] = bp[3 * n];
+        rp[8] = bp[4 * n];
+      }
+      lds_sync();
+    } else {
+      const int c = live ? ln : 0;
+      // every lane loads (lanes >= n read column 0 and discard it): no exec-masked load per column
+      Unroll<0, n>::run([&](auto jc) {
+        constexpr int j = decltype(jc)::value;
+        double t = 0.0;
+        if (j == ln) t = b0;
+        if (j == ln + 2) t = bp2;
+        if (j + 2 == ln) t = bm2;
+        if (j == ln + 4) t = bp4;
+        if (j + 4 == ln) t = bm4;
+        const double pv = P[j * kPS + c];
+        r[j] = live ? pv + t : 0.0;
+      });
+    }
   }
   // Symmetric sweep operator on the rows in r[]: afterwards A^{-1} = -r (row `lane`).
   // Step k: every lane needs its own A[i][k] (register r[k]) and the pivot row A[k][j] =
@@ -182,12 +284,17 @@ struct Ctx {
     bool ok = true;
     Unroll<0, n>::run([&](auto kc) {
       constexpr int k = decltype(kc)::value;
+      // the pivot A[k][k] (lane k's r[k]): by readlane, so 1/d is computed while the column's
+      // broadcast is in flight; then a vector reciprocal (v_rcp_f64 + two Newton steps, within an
+      // ulp of 1/d): no IEEE division sequence on the step's critical path
+#if MPCQP_PIVOT_SGPR
+      const double d = readlane(r[k], k);
+#endif
       double w[4];
-      bcast<kNW>(r[k], w);
-      // the pivot A[k][k] (lane k's r[k]) in every lane, straight from the row copy; then a
-      // vector reciprocal (v_rcp_f64 + two Newton steps, within an ulp of 1/d): no SGPR
-      // round trip and no IEEE division sequence on the step's critical path
-      const double d = dpp<0x150 + (k % 16)>(w[k / 16]);
+      vbcast<MPCQP_BCAST_LDS_SWEEP>(r[k], w);
+#if !MPCQP_PIVOT_SGPR
+      const double d = staged<k, MPCQP_BCAST_LDS_SWEEP>(w);
+#endif
       ok = ok && (d > 0.0) && isfinite(d);
       double inv = __builtin_amdgcn_rcp(d);
       inv = fma(inv, fma(-d, inv, 1.0), inv);
@@ -211,22 +318,22 @@ struct Ctx {
   // the active set.  false (inverse untouched) when 1 + delta c'u is not safely positive.
   __device__ __forceinline__ bool rank1(int tau, int l, double delta) {
     const int lu = __builtin_amdgcn_readfirstlane(l);
-    // the row's coefficients on the variables lu, lu-2, lu-4 (lane lu's e, times D there)
-    const double c0 = readlane(tau == 0 ? E[0] : (tau == 1 ? e1[0] : e2[0]), lu) * readlane(D, lu);
-    const double c1 = lu >= 2 ? readlane(tau == 1 ? e1[1] : (tau == 2 ? e2[1] : 0.0), lu) * readlane(D, lu - 2) : 0.0;
-    const double c2 = lu >= 4 ? readlane(tau == 2 ? e2[2] : 0.0, lu) * readlane(D, lu - 4) : 0.0;
+    // the row's coefficients on the variables lu, lu-2, lu-4 (lane lu's c)
+    const double k0 = readlane(tau == 0 ? c0 : (tau == 1 ? c10 : c20), lu);
+    const double k1 = lu >= 2 ? readlane(tau == 1 ? c11 : (tau == 2 ? c21 : 0.0), lu) : 0.0;
+    const double k2 = lu >= 4 ? readlane(tau == 2 ? c22 : 0.0, lu) : 0.0;
     // u = A^{-1} c: c has at most three entries, so u is three columns of the inverse -- by
     // symmetry the lane's own registers r[lu], r[lu-2], r[lu-4] (A^{-1}[i][j] = -r_i[j])
-    double u = c0 * pick<0, n>(lu);
-    if (lu >= 2) u += c1 * pick<0, n>(lu - 2);
-    if (lu >= 4) u += c2 * pick<0, n>(lu - 4);
+    double u = k0 * pick<0, n>(lu);
+    if (lu >= 2) u += k1 * pick<0, n>(lu - 2);
+    if (lu >= 4) u += k2 * pick<0, n>(lu - 4);
     u = act ? -u : 0.0;
-    const double cu = (c0 * readlane(u, lu) + c1 * readlane(u, lu >= 2 ? lu - 2 : 0)) + c2 * readlane(u, lu >= 4 ? lu - 4 : 0);
+    const double cu = (k0 * readlane(u, lu) + k1 * readlane(u, lu >= 2 ? lu - 2 : 0)) + k2 * readlane(u, lu >= 4 ? lu - 4 : 0);
     const double den = 1.0 + delta * cu;
     if (!(den > kRank1Min) || !isfinite(den)) return false;
     const double m = (delta / den) * u;
     double w[4];
-    bcast<kNW>(u, w);
+    vbcast(u, w);
     Unroll<0, n>::run([&](auto jc) {
       constexpr int j = decltype(jc)::value;
       fmac_bc<j % 16>(r[j], w[j / 16], m);
@@ -255,7 +362,7 @@ struct Ctx {
   // lanes return zero by themselves.
   __device__ __forceinline__ double inv_mul(double v) const {
     double w[4];
-    bcast<kNW>(v, w);
+    vbcast(v, w);
     double a[4] = {0.0, 0.0, 0.0, 0.0};
     Unroll<0, n>::run([&](auto jc) {
       constexpr int j = decltype(jc)::value;
@@ -559,15 +666,31 @@ __device__ __forceinline__ bool setup_qp(const mpcqp_params& p, int b, const dou
   // symmetric Pbar = the lower triangle (row i >= column lane, computed by column `lane`)
   bool finite = isfinite(qv) && isfinite(cscale);
   lds_sync();  // setup's LDS data is dead: Pbar overwrites it
-  if (act) {
+  {
+    constexpr int kPS = SolveSmem<N>::kPS;
     double* Pb = lds.solve.P;
+    if (act) {
 #pragma unroll
-    for (int i = 0; i < n; ++i)
-      if (i >= lane) {  // entry (i, lane) and its mirror (lane, i)
-        Pb[i * n + lane] = Pc[i];
-        Pb[lane * n + i] = Pc[i];
-        finite = finite && isfinite(Pc[i]);
+      for (int i = 0; i < n; ++i)
+        if (i >= lane) {  // entry (i, lane) and its mirror (lane, i)
+          Pb[i * kPS + lane] = Pc[i];
+          Pb[lane * kPS + i] = Pc[i];
+          finite = finite && isfinite(Pc[i]);
+        }
+    } else if (lane == n) {  // the zero padding column
+#pragma unroll
+      for (int i = 0; i < n; ++i) Pb[i * kPS + n] = 0.0;
+    }
+    if (lane < 4) lds.solve.pad0[lane] = 0.0;
+    else if (lane < 8) lds.solve.pad1[lane - 4] = 0.0;
+    if constexpr (n >= 8) {  // form()'s band addresses: save what they hold
+      lds_sync();
+      if (act) {
+        const double* rowp = Pb + lane * (kPS + 1);
+#pragma unroll
+        for (int d = 0; d < 5; ++d) lds.solve.band[d][lane] = rowp[2 * d - 4];
       }
+    }
   }
   double wb[3];
 #pragma unroll
@@ -579,15 +702,19 @@ __device__ __forceinline__ bool setup_qp(const mpcqp_params& p, int b, const dou
   }
   // non-finite data (NaN/inf in x0, ref or u_prev) -> status MPCQP_NUMERICAL_ERROR
   const bool bad_input = wave_any(!finite);
-  C.init(lane, dt, lds.solve);
+  C.init(lane, dt, lds.solve, lds.bc);
   C.qv = qv;
   C.D = D;
   C.cscale = cscale;
-  C.e1[0] = E[1] * k1[0];
-  C.e1[1] = E[1] * k1[1];
-  C.e2[0] = E[2] * k2[0];
-  C.e2[1] = E[2] * k2[1];
-  C.e2[2] = E[2] * k2[2];
+  {  // Cbar's coefficients: row scaling x row coefficient x the column scaling of the variable
+    const double Dm2 = shr2(D), Dm4 = shr2(Dm2);
+    C.c0 = E[0] * D;
+    C.c10 = (E[1] * k1[0]) * D;
+    C.c11 = (E[1] * k1[1]) * Dm2;
+    C.c20 = (E[2] * k2[0]) * D;
+    C.c21 = (E[2] * k2[1]) * Dm2;
+    C.c22 = (E[2] * k2[2]) * Dm4;
+  }
 #pragma unroll
   for (int r = 0; r < 3; ++r) {
     C.E[r] = E[r];
@@ -598,7 +725,7 @@ __device__ __forceinline__ bool setup_qp(const mpcqp_params& p, int b, const dou
   __syncthreads();
   if (dbg) {
     if (act)
-      for (int i = 0; i < n; ++i) dbg[i * n + lane] = lds.solve.P[i * n + lane];
+      for (int i = 0; i < n; ++i) dbg[i * n + lane] = lds.solve.P[i * SolveSmem<N>::kPS + lane];
     double* lf = dbg + state_lane_off(N);
     lf[kFq * kWave + lane] = qv;
     lf[kFD * kWave + lane] = D;
@@ -646,7 +773,10 @@ __device__ __forceinline__ int polish_qp(Ctx<N>& C, double& x, const double zg[3
   double Px = C.Pmul(x);  // P x, carried along the passes
 #pragma unroll
   for (int r = 0; r < 3; ++r) cd[r] = zg[r] > C.hi[r] ? 2 : (zg[r] < C.lo[r] ? 1 : 0);
-  constexpr int kMaxRank1 = n / 2;  // more changed rows than this: refactor (form + sweep)
+#ifndef MPCQP_RANK1_DIV  // development switch: more than n / MPCQP_RANK1_DIV changed rows -> refactor
+#define MPCQP_RANK1_DIV 2
+#endif
+  constexpr int kMaxRank1 = n / MPCQP_RANK1_DIV;  // more changed rows than this: refactor (form + sweep)
   double rwf[3] = {0.0, 0.0, 0.0};  // soft-row weights of the current factorization
   bool have_fact = false;
   for (int pass = 0; pass < max_it; ++pass) {
@@ -678,6 +808,7 @@ __device__ __forceinline__ int polish_qp(Ctx<N>& C, double& x, const double zg[3
           const int l = __builtin_ctzll(m);
           m &= m - 1;
           refac = !C.rank1(r, l, readlane(rw[r] - rwf[r], l));
+          ++C.n_r1;
         }
       }
       T.end(1);
@@ -689,6 +820,7 @@ __device__ __forceinline__ int polish_qp(Ctx<N>& C, double& x, const double zg[3
       T.begin();
       const bool okf = C.sweep();
       T.end(1);
+      ++C.n_full;
       if (wave_any(!okf)) {
         result = -1;
         break;
@@ -831,13 +963,18 @@ __device__ __forceinline__ int admm_qp(const mpcqp_params& p, Ctx<N>& C, bool ba
       }
     }
     bool refactor = false;
-    double prox_a[3], prox_b[3];  // zn = (rho vv + 2 w bnd) / (rho + 2 w)
+    // The z-update is the prox of the eliminated slack's penalty w dist(z, [lo, hi])^2:
+    //   zn = vv - pb (vv - clamp(vv, lo, hi)),  pb = 2w / (rho + 2w)
+    // (= (rho vv + 2 w bnd) / (rho + 2 w) outside the bounds, vv inside), and the dual update
+    // y + rho (v - zn) with vv = v + y / rho is exactly rho pb (vv - clamp): no selects, and no
+    // cancellation of y against rho (v - zn).
+    double pb[3], rpb[3];
 #pragma unroll
     for (int r = 0; r < 3; ++r) {
-      prox_a[r] = rho / (rho + 2.0 * C.wb[r]);
-      prox_b[r] = 2.0 * C.wb[r] / (rho + 2.0 * C.wb[r]);
+      pb[r] = 2.0 * C.wb[r] / (rho + 2.0 * C.wb[r]);
+      rpb[r] = rho * pb[r];
     }
-    const double ir = 1.0 / rho;
+    const double ir = 1.0 / rho, oma = 1.0 - alpha;
     while (!refactor && it < p.max_iter) {
       ++it;
       C.opaque();
@@ -846,20 +983,18 @@ __device__ __forceinline__ int admm_qp(const mpcqp_params& p, Ctx<N>& C, bool ba
 #pragma unroll
       for (int r = 0; r < 3; ++r) tmp[r] = rho * z[r] - y[r];
       const double rhs = C.CTmul(tmp) + sg * x - C.qv;
-      const double xt = C.inv_mul(rhs);
-      double zt[3];
-      C.Cmul(xt, zt);
-      x = alpha * xt + (1.0 - alpha) * x;
+      // relaxation folded into the step: xa = alpha xt, Cbar xa = alpha Cbar xt
+      const double xa = alpha * C.inv_mul(rhs);
+      double za[3];
+      C.Cmul(xa, za);
+      x = xa + oma * x;
 #pragma unroll
       for (int r = 0; r < 3; ++r) {
-        const double v = alpha * zt[r] + (1.0 - alpha) * z[r];
+        const double v = za[r] + oma * z[r];
         const double vv = v + y[r] * ir;
-        // branch-free: both clamped candidates, then selects
-        const double zhi = prox_a[r] * vv + prox_b[r] * C.hi[r];
-        const double zlo = prox_a[r] * vv + prox_b[r] * C.lo[r];
-        const double zn = vv > C.hi[r] ? zhi : (vv < C.lo[r] ? zlo : vv);
-        y[r] = y[r] + rho * (v - zn);
-        z[r] = zn;
+        const double d = vv - fmin(fmax(vv, C.lo[r]), C.hi[r]);
+        z[r] = vv - pb[r] * d;
+        y[r] = rpb[r] * d;
       }
       T.end(2);
       if (it % p.check_termination == 0 || it == p.max_iter) {
@@ -1008,6 +1143,8 @@ __device__ __forceinline__ void finish_qp(const mpcqp_params& p, int b, const do
   }
   T2.end(0);
   T2.flush(12);  // g_stamps[12]: polish phase of k_finish
+  Stamps T3;
+  T3.begin();
   if (wave_any(!isfinite(x))) bad = true;
   int status;
   if (bad) {
@@ -1120,6 +1257,8 @@ __device__ __forceinline__ void finish_qp(const mpcqp_params& p, int b, const do
       ab[3 * N + 1 + lane] = d > p.du_bounds[2 * cc + 1] ? 2 : (d < p.du_bounds[2 * cc] ? 1 : 0);
     }
   }
+  T3.end(0);
+  T3.flush(13);  // g_stamps[13]: status + outputs
   if (lane == 0) {
     statuso[b] = status;
     if (iterso) {
@@ -1164,6 +1303,8 @@ __global__ __launch_bounds__(kWave, kSolveWavesPerEU<N>) void k_solve(mpcqp_para
   if (b >= B || (mask && !mask[b])) return;
   double* dbg = p.debug_state ? state + (size_t)b * state_stride(N) : nullptr;
   const uint64_t t_start = __builtin_amdgcn_s_memtime();
+  Stamps TK;
+  TK.begin();
   Ctx<N> C;
   const bool bad = setup_qp<N>(p, b, model, in_x0, in_ref, in_up, C, sm, state + (size_t)b * state_stride(N), dbg);
   double x = 0.0, z[3] = {0.0, 0.0, 0.0};
@@ -1171,8 +1312,14 @@ __global__ __launch_bounds__(kWave, kSolveWavesPerEU<N>) void k_solve(mpcqp_para
   if (p.method == MPCQP_METHOD_ADMM) flag = admm_qp<N>(p, C, bad, x, z, it, nfact, pol_it, n_ls, dbg);
   finish_qp<N>(p, b, model, in_x0, in_ref, in_up, sm.model, C, x, z, flag, it, nfact, pol_it, n_ls, u0o, Xo, Uo, statuso, iterso,
                activeo);
-  if (dbg && threadIdx.x == 0)  // this wave's cycles, start to finish (tools/qp_cycles.py)
+  TK.end(0);
+  TK.flush(22);  // g_stamps[22]: the whole QP
+  if (dbg && threadIdx.x == 0) {  // this wave's cycles, start to finish, and its work (tools/qp_cycles.py)
     dbg[state_scal_off(N) + 4] = (double)(__builtin_amdgcn_s_memtime() - t_start);
+    dbg[state_scal_off(N) + 5] = (double)C.n_full;  // polish factorizations from scratch
+    dbg[state_scal_off(N) + 6] = (double)C.n_r1;    // polish rank-1 updates
+    dbg[state_scal_off(N) + 7] = (double)t_start;
+  }
 }
 
 }  // namespace

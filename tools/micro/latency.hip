@@ -89,6 +89,23 @@ __global__ __launch_bounds__(64) void k(const double* __restrict__ in, double* _
       double w[4];
       bcast<3>(v, w);
       v = (w[0] + w[1] + w[2]) * 1e-3;
+    } else if constexpr (V == 14) {  // 16 dependent wave_shr:1 DPP moves (lo + hi)
+#pragma unroll
+      for (int j = 0; j < 16; ++j) v = dpp<kWaveShr1>(v);
+    } else if constexpr (V == 15) {  // 16 dependent select + fma (prox-like)
+#pragma unroll
+      for (int j = 0; j < 16; ++j) v = (v > u ? fma(v, 0.5, u) : v * 1.25);
+    } else if constexpr (V == 16) {  // 16 dependent permlane32 swaps
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        int lo = __double2loint(v), hi = __double2hiint(v);
+        const auto a = __builtin_amdgcn_permlane32_swap(lo, lo, false, false);
+        const auto b = __builtin_amdgcn_permlane32_swap(hi, hi, false, false);
+        v = __hiloint2double(b[0], a[0]);
+      }
+    } else if constexpr (V == 17) {  // 16 dependent readlane(63) -> v_add (SGPR round trip)
+#pragma unroll
+      for (int j = 0; j < 16; ++j) v = readlane(v, 63) + v;
     } else if constexpr (V == 8) {  // 16 dependent shr2 (4 DPP movs each)
 #pragma unroll
       for (int j = 0; j < 16; ++j) v = shr2(v) + 1.0;
@@ -155,6 +172,10 @@ int main() {
     run<11>("bcast + 40 fmac_dpp 8 chains", 1, din, dout, dc, waves, waves);
     run<12>("bcast + 40 fmac_dpp 2 chains", 1, din, dout, dc, waves, waves);
     run<13>("bcast alone (+2 adds)", 1, din, dout, dc, waves, waves);
+    run<14>("wave_shr1 dpp move (per move)", 16, din, dout, dc, waves, waves);
+    run<15>("select + fma (per step)", 16, din, dout, dc, waves, waves);
+    run<16>("permlane32 swap (per swap)", 16, din, dout, dc, waves, waves);
+    run<17>("readlane + add (per step)", 16, din, dout, dc, waves, waves);
   }
   return 0;
 }

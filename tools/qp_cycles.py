@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Development tool: per-QP wave cycles (s_memtime, start to finish, written with debug_state)
 against the QP's own work counters, fitted as cycles ~ c0 + c1*ADMM its + c2*factorizations +
-c3*polish its + c4*line-search trials + c5*checks.  The marginal cost of each unit of work on the
+c3*checks + ... (polish factorizations, rank-1 updates, passes, line-search trials).  The marginal cost of each unit of work on the
 critical path of one wave, at the batch's real occupancy.
 
     python tools/qp_cycles.py [--batch 4096] [--lone 256]
@@ -41,18 +41,34 @@ def run(B, stride_pick=1):
     hip.hipMemcpy(ctypes.c_void_p(st.data_ptr()), ctypes.c_void_p(ptr), ctypes.c_size_t(B * SS * 8), 3)
     cyc = st[:, L.mpcqp_state_stride(20) - 8 + 4].cpu().numpy() if False else None
     off = (4 * 20 * 20 + 7) // 8 * 8 + 15 * 64 + 4
-    cyc = st[:, off].cpu().numpy()
+    sc = st[:, off:off + 4].cpu().numpy()  # cycles, polish full factorizations, rank-1 updates, start time
     it = ctrl._iters[:B].cpu().numpy().astype(float)
-    return cyc, it
+    return sc, it
 
 
-def fit(cyc, it):
+def fit(sc, it):
+    cyc, full, r1 = sc[:, 0], sc[:, 1], sc[:, 2]
     checks = np.floor(it[:, 0] / 25) + (it[:, 0] % 25 > 0)
-    A = np.column_stack([np.ones(len(cyc)), it[:, 0], it[:, 2], it[:, 1], it[:, 3], checks])
+    admm_fact = it[:, 2] - it[:, 1]  # nfact counts the ADMM factorizations and every polish pass
+    A = np.column_stack([np.ones(len(cyc)), it[:, 0], checks, admm_fact, full, r1, it[:, 1], it[:, 3]])
     coef, *_ = np.linalg.lstsq(A, cyc, rcond=None)
     pred = A @ coef
-    names = ["const", "admm_it", "factorization", "polish_it", "ls_trial", "check"]
-    return {n: round(float(c)) for n, c in zip(names, coef)}, float(np.corrcoef(pred, cyc)[0, 1])
+    names = ["const", "admm_it", "check", "admm_factorization", "polish_full_factorization", "rank1_update",
+             "polish_pass", "ls_trial"]
+    means = dict(zip(names[1:], A[:, 1:].mean(axis=0).round(3).tolist()))
+    share = {n: round(float(c * A[:, i].mean() / cyc.mean()), 3) for i, (n, c) in enumerate(zip(names, coef))}
+    return {n: round(float(c)) for n, c in zip(names, coef)}, float(np.corrcoef(pred, cyc)[0, 1]), means, share
+
+
+def timeline(sc):
+    """Occupancy of the batch's waves over the kernel: the span from the first start to the last end
+    against the summed wave lifetimes (s_memtime is one clock per XCD; good to a few hundred cycles)."""
+    start = sc[:, 3] - sc[:, 3].min()
+    end = start + sc[:, 0]
+    span = end.max()
+    return {"span_cycles": float(span), "sum_wave_cycles": float(sc[:, 0].sum()),
+            "last_start": float(start.max()), "end_p50": float(np.percentile(end, 50)),
+            "end_p90": float(np.percentile(end, 90)), "end_p99": float(np.percentile(end, 99))}
 
 
 def main():
@@ -62,12 +78,15 @@ def main():
     a = ap.parse_args()
     out = {}
     for name, B, stride in (("full", a.batch, 1), ("lone", a.lone, 4096 // a.lone)):
-        cyc, it = run(B, stride)
-        coef, r = fit(cyc, it)
+        sc, it = run(B, stride)
+        cyc = sc[:, 0]
+        coef, r, means, share = fit(sc, it)
         w = int(np.argmax(cyc))
         out[name] = {"batch": B, "cycles_mean": float(cyc.mean()), "cycles_max": float(cyc.max()),
-                     "p99": float(np.percentile(cyc, 99)), "fit": coef, "fit_r": r,
-                     "slowest_qp_iters": it[w].tolist(), "slowest_qp_cycles": float(cyc[w])}
+                     "p99": float(np.percentile(cyc, 99)), "fit": coef, "fit_r": r, "work_means": means,
+                     "cycle_share": share, "timeline": timeline(sc),
+                     "slowest_qp_iters": it[w].tolist(), "slowest_qp_work": sc[w, 1:3].tolist(),
+                     "slowest_qp_cycles": float(cyc[w])}
     print(json.dumps(out, indent=1))
 
 

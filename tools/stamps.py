@@ -26,6 +26,7 @@ sys.path.insert(0, str(ROOT / "rrt-mpc_amd"))
 
 NAMES = {0: "admm.form", 1: "admm.sweep", 2: "admm.iteration", 3: "admm.check", 4: "admm.total",
          8: "polish.form", 9: "polish.sweep", 10: "polish.solve", 11: "polish.linesearch", 12: "polish.total",
+         13: "finish.outputs", 22: "qp.total",
          16: "setup.load_prefix", 17: "setup.condense", 18: "setup.unscaled", 19: "setup.ruiz", 20: "setup.write",
          21: "setup.total"}
 
