@@ -20,8 +20,8 @@ from __future__ import annotations
 
 import ctypes
 import time
-from dataclasses import dataclass, field
-from typing import Dict, List, Optional
+from dataclasses import dataclass, field, fields
+from typing import Callable, Dict, List, Optional, Sequence, Tuple
 
 import numpy as np
 
@@ -178,4 +178,56 @@ class Swarm:
                            last_replan_path=last_paths, inputs=r.inputs, timings=t)
 
 
-__all__ = ["Swarm", "SwarmResult", "replan_seed", "REPLAN_SEED_STRIDE"]
+# ------------------------------------------------------------------ multi-GPU: vehicles sharded over ranks
+# The vehicles of the swarm are independent (the reference tracks each one alone,
+# control_stage.py:100-150; nothing couples two vehicles), so config 5 on G GPUs gives each rank a
+# contiguous block of vehicles -- with the vehicles' own seeds, so every vehicle does exactly what it
+# does in a one-GPU run -- and the only collective is the gather of the per-vehicle results at the end
+# (no data-path exchange: weak scaling in the vehicles, strong scaling of a fixed swarm).
+
+def shard_vehicles(V: int, world: int, rank: int) -> Tuple[int, int]:
+    """[lo, hi) of rank's contiguous block; block sizes differ by at most one (bench.shard_bounds)."""
+    base, extra = divmod(int(V), int(world))
+    lo = rank * base + min(rank, extra)
+    return lo, lo + base + (1 if rank < extra else 0)
+
+
+_PER_VEHICLE_ARRAYS = ("phase", "steps", "replans", "planned", "replan_steps", "last_replan_start")
+_PER_VEHICLE_LISTS = ("states", "paths", "last_replan_path", "inputs")
+
+
+def merge_swarm_results(parts: Sequence[SwarmResult]) -> SwarmResult:
+    """Rank-ordered shard results -> the swarm's result in vehicle order; timings: max over ranks
+    (the ranks run concurrently, the slowest one sets the swarm's wall time)."""
+    parts = [p for p in parts if p is not None]
+    kw = {}
+    for f in fields(SwarmResult):
+        vals = [getattr(p, f.name) for p in parts]
+        if f.name in _PER_VEHICLE_ARRAYS:
+            vals = [v for v in vals if v is not None and len(v)]
+            kw[f.name] = np.concatenate(vals) if vals else None
+        elif f.name in _PER_VEHICLE_LISTS:
+            kw[f.name] = [x for v in vals for x in v]
+        elif f.name == "timings":
+            keys = sorted({k for v in vals for k in v})
+            kw[f.name] = {k: max(v.get(k, 0.0) for v in vals) for k in keys}
+    return SwarmResult(**kw)
+
+
+def run_swarm_sharded(run: Callable[..., SwarmResult], starts, goals, seeds, *, rank: int, world: int,
+                      all_gather_object: Callable[[list, object], None], **kwargs) -> SwarmResult:
+    """Run rank's block of the swarm with ``run`` (``Swarm.run`` of this rank's device) and gather
+    every rank's result: each rank returns the whole swarm's result, in vehicle order."""
+    starts = np.asarray(starts, dtype=float).reshape(-1, 2)
+    goals = np.asarray(goals, dtype=float).reshape(-1, 2)
+    V = len(starts)
+    seeds = np.arange(V) if seeds is None else np.asarray(seeds)
+    lo, hi = shard_vehicles(V, world, rank)
+    local = run(starts[lo:hi], goals[lo:hi], seeds=seeds[lo:hi], **kwargs) if hi > lo else None
+    parts: list = [None] * world
+    all_gather_object(parts, local)
+    return merge_swarm_results(parts)
+
+
+__all__ = ["Swarm", "SwarmResult", "replan_seed", "REPLAN_SEED_STRIDE", "shard_vehicles", "merge_swarm_results",
+           "run_swarm_sharded"]

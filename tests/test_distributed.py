@@ -107,3 +107,70 @@ def test_weak_shards_are_contiguous_and_cover_the_batch():
     parts = [bench.make_batch("config3", 8, 4, r) for r in range(4)]
     np.testing.assert_array_equal(np.concatenate([p[0] for p in parts]), whole[0])
     np.testing.assert_array_equal(np.concatenate([p[1] for p in parts]), whole[1])
+
+
+def _stub_swarm_run(starts, goals, seeds, sim_steps=None):
+    """A deterministic stand-in for Swarm.run (no GPU here): every per-vehicle field a function of
+    that vehicle's own inputs, so a sharded run must reassemble the single-process result exactly."""
+    sys.path.insert(0, str(ROOT / "rrt-mpc_amd"))
+    from mpcqp.pipeline.swarm import SwarmResult
+
+    V = len(starts)
+    seeds = np.asarray(seeds)
+    states = [np.array([[s[0], s[1], float(k)] for k in range(int(sd) % 5 + 1)]) for s, sd in zip(starts, seeds)]
+    return SwarmResult(states=states, phase=(seeds % 3).astype(np.int32), steps=(seeds * 7 % 11).astype(np.int32),
+                       replans=(seeds % 2).astype(np.int64), planned=seeds % 4 != 0,
+                       paths=[[tuple(s), tuple(g)] for s, g in zip(starts, goals)],
+                       replan_steps=np.stack([seeds, -seeds], axis=1).astype(np.int32),
+                       last_replan_start=np.asarray(starts, float), last_replan_path=[None] * V,
+                       inputs=[np.full((2, 2), float(sd)) for sd in seeds],
+                       timings={"plan_s": 0.1 * len(starts), "track_replan_s": float(seeds.sum())})
+
+
+def _swarm_worker(rank, world, port, V, out_dir):
+    for p in (ROOT / "rrt-mpc_amd", ROOT):
+        sys.path.insert(0, str(p))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    import pickle
+
+    import torch.distributed as dist
+
+    from mpcqp.pipeline.swarm import run_swarm_sharded
+
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    rng = np.random.default_rng(3)
+    starts, goals = rng.uniform(0, 80, (V, 2)), rng.uniform(0, 80, (V, 2))
+    res = run_swarm_sharded(_stub_swarm_run, starts, goals, np.arange(V) + 100, rank=rank, world=world,
+                            all_gather_object=dist.all_gather_object, sim_steps=5)
+    with open(Path(out_dir) / f"swarm_{rank}.pkl", "wb") as f:
+        pickle.dump(res, f)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("world,V", [(2, 100), (3, 7), (4, 3)])
+def test_sharded_swarm_matches_single_process(tmp_path, world, V):
+    """Config 5 over `world` ranks (gloo): contiguous vehicle blocks (3 vehicles over 4 ranks leaves one
+    rank empty), one all_gather_object of the shard results; every rank gets the single-process result
+    in vehicle order, timings the max over ranks."""
+    import pickle
+
+    sys.path.insert(0, str(ROOT / "rrt-mpc_amd"))
+    from mpcqp.pipeline.swarm import shard_vehicles
+
+    mp.start_processes(_swarm_worker, args=(world, _free_port(), V, str(tmp_path)), nprocs=world,
+                       start_method="spawn", join=True)
+    rng = np.random.default_rng(3)
+    starts, goals = rng.uniform(0, 80, (V, 2)), rng.uniform(0, 80, (V, 2))
+    full = _stub_swarm_run(starts, goals, np.arange(V) + 100)
+    for r in range(world):
+        with open(tmp_path / f"swarm_{r}.pkl", "rb") as f:
+            got = pickle.load(f)
+        for k in ("phase", "steps", "replans", "planned", "replan_steps", "last_replan_start"):
+            np.testing.assert_array_equal(getattr(got, k), getattr(full, k), err_msg=k)
+        assert len(got.states) == V and all(np.array_equal(a, b) for a, b in zip(got.states, full.states))
+        assert all(np.array_equal(a, b) for a, b in zip(got.inputs, full.inputs))
+        assert got.paths == full.paths
+        blocks = [shard_vehicles(V, world, q) for q in range(world)]
+        assert got.timings["plan_s"] == pytest.approx(max(0.1 * (hi - lo) for lo, hi in blocks))

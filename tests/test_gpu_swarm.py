@@ -185,3 +185,39 @@ def test_per_step_replan_100_vehicles(cuda, golden):
     reached = res.phase == _lib.FLEET_GOAL
     for v in np.flatnonzero(reached):  # goal test of control_stage.py:147-150 on the last state
         assert np.hypot(*(res.states[v][-1, :2] - goals[v])) < 8.0
+
+
+def test_sharded_swarm_equals_one_swarm(cuda, golden):
+    """Config 5 sharded by vehicle (run_swarm_sharded, the multi-GPU path): three ranks emulated in
+    one process on one GPU, each running its contiguous block on its own Swarm; the gathered result
+    equals the one-Swarm run of all vehicles exactly (steps, phases, replans, every state), with the
+    replan trigger live (2.5 px)."""
+    from mpcqp.pipeline.swarm import run_swarm_sharded, shard_vehicles
+
+    occ = golden("default_plan.npz")["occupancy"]
+    V, world = 40, 3
+    starts, goals = _pairs(occ, V, 21)
+    one = _swarm(occ, V, 200, replan_distance=2.5).run(starts, goals, seeds=np.arange(V), check_every=25)
+    shards = []
+    for r in range(world):  # each "rank": its own Swarm sized to its block
+        lo, hi = shard_vehicles(V, world, r)
+        sw = _swarm(occ, hi - lo, 200, replan_distance=2.5)
+        shards.append(run_swarm_sharded(sw.run, starts, goals, np.arange(V), rank=r, world=world,
+                                        all_gather_object=lambda out, obj, r=r: out.__setitem__(r, obj),
+                                        check_every=25))
+    # every rank gathered only its own part here; merging the three reproduces the all-gather
+    from mpcqp.pipeline.swarm import merge_swarm_results
+
+    parts = []
+    for r in range(world):
+        lo, hi = shard_vehicles(V, world, r)
+        p = shards[r]
+        assert len(p.steps) == hi - lo
+        parts.append(p)
+    got = merge_swarm_results(parts)
+    assert one.replans.sum() > 0, "the trigger should fire at 2.5 px"
+    np.testing.assert_array_equal(got.steps, one.steps)
+    np.testing.assert_array_equal(got.phase, one.phase)
+    np.testing.assert_array_equal(got.replans, one.replans)
+    np.testing.assert_array_equal(got.planned, one.planned)
+    assert all(np.array_equal(a, b) for a, b in zip(got.states, one.states))

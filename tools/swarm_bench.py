@@ -5,6 +5,15 @@ trigger of mpcqp/pipeline/swarm.py.  Also times the planner alone (trees/s, batc
 reference algorithm restated in Python on one host core) and the inflation kernel.
 
     python tools/swarm_bench.py [--vehicles 100 1024] [--steps 300]
+
+Multi-GPU (BASELINE config 5 on 8 GPUs): vehicles sharded over ranks (mpcqp.pipeline.swarm
+.run_swarm_sharded), one process per GPU, the per-vehicle results gathered at the end:
+
+    python -m torch.distributed.run --nproc-per-node G --master-addr 127.0.0.1 tools/swarm_bench.py \
+        --distributed [--backend nccl|gloo] [--vehicles 100]
+
+Rank 0 then also runs the whole swarm alone on its GPU and checks that every vehicle's closed
+loop (steps, phase, replans, states) is identical to the sharded run.
 """
 from __future__ import annotations
 
@@ -33,6 +42,60 @@ def pairs(occ, V, seed):
     return np.array(s), np.array(g)
 
 
+def distributed(a) -> None:
+    import os
+
+    import torch
+    import torch.distributed as dist
+
+    from mpcqp.config import MPCConfig
+    from mpcqp.pipeline.swarm import Swarm, run_swarm_sharded, shard_vehicles
+    from mpcqp.planning.rrt_star import default_planner_parameters
+
+    rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
+    local = int(os.environ.get("LOCAL_RANK", rank))
+    dev = torch.device("cuda", local % torch.cuda.device_count())
+    torch.cuda.set_device(dev)
+    dist.init_process_group(a.backend, rank=rank, world_size=world)
+    d = np.load(ROOT / "rrt-mpc_amd" / "mpcqp" / "data" / "default_plan.npz")
+    occ = d["occupancy"]
+    prm = default_planner_parameters()
+    mpc = MPCConfig(horizon=15, sim_steps=a.steps)
+    for V in a.vehicles:
+        starts, goals = pairs(occ, V, 5)
+        lo, hi = shard_vehicles(V, world, rank)
+        sw = Swarm(occ, mpc, prm, map_resolution=0.8, max_vehicles=max(hi - lo, 1), device=dev,
+                   replan_distance=a.replan_distance, max_replans=a.max_replans)
+        sw.run(starts[:1], goals[:1], seeds=np.arange(1), sim_steps=5)  # warm
+        torch.cuda.synchronize(dev)
+        dist.barrier()
+        t0 = time.perf_counter()
+        res = run_swarm_sharded(sw.run, starts, goals, np.arange(V), rank=rank, world=world,
+                                all_gather_object=dist.all_gather_object, check_every=50)
+        torch.cuda.synchronize(dev)
+        dist.barrier()
+        dt = time.perf_counter() - t0
+        t = torch.tensor([dt], dtype=torch.float64, device=dev if a.backend == "nccl" else "cpu")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        if rank == 0:
+            one = Swarm(occ, mpc, prm, map_resolution=0.8, max_vehicles=V, device=dev,
+                        replan_distance=a.replan_distance, max_replans=a.max_replans)
+            ref = one.run(starts, goals, seeds=np.arange(V), check_every=50)
+            same = (np.array_equal(res.steps, ref.steps) and np.array_equal(res.phase, ref.phase)
+                    and np.array_equal(res.replans, ref.replans)
+                    and all(np.array_equal(x, y) for x, y in zip(res.states, ref.states)))
+            print(json.dumps({"vehicles": V, "ranks": world, "backend": a.backend, "seconds": float(t.item()),
+                              "vehicle_steps": int(res.steps.sum()),
+                              "vehicle_steps_per_s": int(res.steps.sum()) / float(t.item()),
+                              "goal_reached": int((res.phase == 1).sum()), "replans": int(res.replans.sum()),
+                              "vehicles_per_rank": [hi_ - lo_ for lo_, hi_ in
+                                                    (shard_vehicles(V, world, q) for q in range(world))],
+                              "identical_to_one_process_run": bool(same),
+                              "one_process_seconds_same_gpu": sum(ref.timings.values())}), flush=True)
+        dist.barrier()
+    dist.destroy_process_group()
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--vehicles", type=int, nargs="+", default=[100, 1024])
@@ -40,7 +103,12 @@ def main() -> None:
     ap.add_argument("--replan-distance", type=float, default=5.5,
                     help="per-step off-track trigger (px); the default fires for a share of the vehicles")
     ap.add_argument("--max-replans", type=int, default=2)
+    ap.add_argument("--distributed", action="store_true", help="vehicles sharded over torch.distributed ranks")
+    ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"])
     a = ap.parse_args()
+    if a.distributed:
+        distributed(a)
+        return
     import torch
 
     from mpcqp.config import MPCConfig
