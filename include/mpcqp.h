@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define MPCQP_ABI_VERSION 4
+#define MPCQP_ABI_VERSION 5
 
 /* error codes (function return values) */
 #define MPCQP_OK 0
@@ -104,6 +104,12 @@ typedef struct mpcqp_params {
   int32_t polish_attempt_max_iter; /* 30 */
   double polish_near;         /* 3: also attempt the polish from iteration 2*check_termination on when
                                  both residuals are within this factor of their tolerances; 0 off */
+  int32_t reproducible;       /* 0: one wave per QP for N < MPCQP_WIDE_MIN_HORIZON (fast; its wave-tree
+                                 reductions round differently from the C restatement).  1: every
+                                 horizon runs the workgroup-per-QP kernel, which is oracle/mpcqp_cpu.c
+                                 parallelised without changing a floating-point operation: solutions,
+                                 statuses and every iteration counter bit-identical to the C code given
+                                 the same LTV model.  Fixed at mpcqp_create (it sizes the workspace). */
 } mpcqp_params;
 
 typedef struct mpcqp_ws mpcqp_ws;
@@ -348,6 +354,8 @@ const double* mpcqp_model_buffer(const mpcqp_ws* ws);
 int mpcqp_model_stride(int horizon);
 const double* mpcqp_state_buffer(const mpcqp_ws* ws);
 int mpcqp_state_stride(int horizon);
+/* Per-QP doubles of this workspace's state buffer (its kernel: mpcqp_params.reproducible). */
+int mpcqp_ws_state_stride(const mpcqp_ws* ws);
 
 /* Test hook: applies the kernels' 64-lane wavefront primitives (DPP prefix/suffix scans,
  * reductions, lane shifts) to in[64] -> out[10 x 64] on the device. */

@@ -51,6 +51,7 @@ class CParams(ctypes.Structure):
         ("polish_from", ctypes.c_int32),
         ("polish_attempt_max_iter", ctypes.c_int32),
         ("polish_near", ctypes.c_double),
+        ("reproducible", ctypes.c_int32),  # product-side kernel choice; the C restatement ignores it
     ]
 
 

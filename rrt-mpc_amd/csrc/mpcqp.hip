@@ -82,8 +82,8 @@ const mpcqp::launcher_t kLaunchers[MPCQP_WIDE_MIN_HORIZON] = {
 
 // per-QP doubles of the solver state buffer (debug state of the one-wave kernel, the workspace
 // of the long-horizon kernel)
-size_t ws_state_stride(int N) {
-  return N >= MPCQP_WIDE_FROM ? mpcqp::wide_stride(N) : (size_t)state_stride(N);
+size_t ws_state_stride(int N, bool wide) {
+  return wide ? mpcqp::wide_stride(N) : (size_t)state_stride(N);
 }
 
 thread_local std::string g_err;
@@ -94,7 +94,8 @@ int check_params(const mpcqp_params* p) {
   if (p->horizon < 1 || p->horizon > MPCQP_MAX_HORIZON)
     return fail(MPCQP_E_HORIZON, "horizon " + std::to_string(p->horizon) + " outside [1, " +
                                      std::to_string(MPCQP_MAX_HORIZON) + "]");
-  if (!mpcqp::launcher(p->horizon)) return fail(MPCQP_E_HORIZON, "horizon not compiled into this build");
+  if (!mpcqp::launcher(*p)) return fail(MPCQP_E_HORIZON, "horizon not compiled into this build");
+  if (p->reproducible != 0 && p->reproducible != 1) return fail(MPCQP_E_ARG, "reproducible must be 0 or 1");
   if (!(p->dt > 0.0) || !(p->wheelbase_px > 0.0)) return fail(MPCQP_E_ARG, "dt and wheelbase_px must be > 0");
   if (p->method != MPCQP_METHOD_ADMM && p->method != MPCQP_METHOD_NEWTON) return fail(MPCQP_E_ARG, "bad method");
   if (p->max_iter < 1 || p->check_termination < 1 || p->adaptive_rho_interval < 1 || p->polish_max_iter < 0 ||
@@ -112,9 +113,12 @@ int fail(int code, const std::string& msg) {
   g_err = msg;
   return code;
 }
-launcher_t launcher(int horizon) {
-  if (horizon >= MPCQP_WIDE_FROM && horizon <= MPCQP_MAX_HORIZON) return &launch_solve_wide;
-  return horizon >= 1 && horizon < MPCQP_WIDE_MIN_HORIZON ? kLaunchers[horizon] : nullptr;
+bool wide_solve(const mpcqp_params& p) { return p.horizon >= MPCQP_WIDE_FROM || p.reproducible != 0; }
+launcher_t launcher(const mpcqp_params& p) {
+  const int horizon = p.horizon;
+  if (horizon < 1 || horizon > MPCQP_MAX_HORIZON) return nullptr;
+  if (wide_solve(p)) return &launch_solve_wide;
+  return horizon < MPCQP_WIDE_MIN_HORIZON ? kLaunchers[horizon] : nullptr;
 }
 }  // namespace mpcqp
 
@@ -146,7 +150,7 @@ int mpcqp_create(const mpcqp_params* p, int max_batch, int device, mpcqp_ws** ws
   w->state = nullptr;
   w->in_x0 = w->in_ref = w->in_up = nullptr;
   const size_t mbytes = sizeof(double) * (size_t)model_stride(p->horizon) * (size_t)max_batch;
-  const size_t sbytes = sizeof(double) * ws_state_stride(p->horizon) * (size_t)max_batch;
+  const size_t sbytes = sizeof(double) * ws_state_stride(p->horizon, mpcqp::wide_solve(*p)) * (size_t)max_batch;
   e = hipMalloc(&w->model, mbytes);
   if (e == hipSuccess) e = hipMalloc(&w->state, sbytes);
   if (e != hipSuccess) {
@@ -164,6 +168,7 @@ int mpcqp_set_params(mpcqp_ws* ws, const mpcqp_params* p) {
   int rc = check_params(p);
   if (rc) return rc;
   if (p->horizon != ws->p.horizon) return fail(MPCQP_E_HORIZON, "set_params cannot change the horizon");
+  if (p->reproducible != ws->p.reproducible) return fail(MPCQP_E_ARG, "set_params cannot change reproducible");
   ws->p = *p;
   return MPCQP_OK;
 }
@@ -184,7 +189,7 @@ int mpcqp_build(mpcqp_ws* ws, int B, const double* x0, const double* ref, const 
   if (B == 0) return MPCQP_OK;
   // The one-wave solve builds the model itself (K1 fused into k_solve: the model block never
   // touches HBM); the K1 kernel runs only for the long-horizon solve and for inspection builds.
-  if (ws->p.horizon < MPCQP_WIDE_FROM && !ws->p.debug_state) {
+  if (!mpcqp::wide_solve(ws->p) && !ws->p.debug_state) {
     ws->in_x0 = x0;
     ws->in_ref = ref;
     ws->in_up = u_prev;
@@ -207,7 +212,7 @@ int mpcqp_solve(mpcqp_ws* ws, int B, double* u0, double* X, double* U, int32_t* 
   L.x0 = ws->in_x0;
   L.ref = ws->in_ref;
   L.u_prev = ws->in_up;
-  mpcqp::launcher(ws->p.horizon)(s, L);
+  mpcqp::launcher(ws->p)(s, L);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return fail(MPCQP_E_HIP, std::string("k_solve launch: ") + hipGetErrorString(e));
   return MPCQP_OK;
@@ -217,7 +222,12 @@ const double* mpcqp_model_buffer(const mpcqp_ws* ws) { return ws ? ws->model : n
 
 const double* mpcqp_state_buffer(const mpcqp_ws* ws) { return ws ? ws->state : nullptr; }
 
-int mpcqp_state_stride(int horizon) { return (int)ws_state_stride(horizon); }
+int mpcqp_state_stride(int horizon) { return (int)ws_state_stride(horizon, horizon >= MPCQP_WIDE_FROM); }
+
+int mpcqp_ws_state_stride(const mpcqp_ws* ws) {
+  if (!ws) return fail(MPCQP_E_ARG, "null ws");
+  return (int)ws_state_stride(ws->p.horizon, mpcqp::wide_solve(ws->p));
+}
 
 int mpcqp_debug_stamps(unsigned long long* out32, int reset) {
 #ifdef MPCQP_STAMPS

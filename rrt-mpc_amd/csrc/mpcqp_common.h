@@ -271,8 +271,10 @@ void launch_solve(hipStream_t s, const Launch& L);
 // per QP, L.state = its workspace (wide_stride(N) doubles per QP)
 void launch_solve_wide(hipStream_t s, const Launch& L);
 size_t wide_stride(int horizon);
-// launcher of horizon N (nullptr when not compiled in); defined in mpcqp.hip
-launcher_t launcher(int horizon);
+// the solve of this parameter block runs the workgroup-per-QP kernel (long horizon or reproducible)
+bool wide_solve(const mpcqp_params& p);
+// launcher of the parameter block's horizon / kernel (nullptr when not compiled in); defined in mpcqp.hip
+launcher_t launcher(const mpcqp_params& p);
 // records msg as mpcqp_last_error() of the calling thread and returns code; defined in mpcqp.hip
 int fail(int code, const std::string& msg);
 }  // namespace mpcqp

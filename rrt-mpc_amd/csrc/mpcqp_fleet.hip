@@ -137,8 +137,8 @@ int check_fleet(const mpcqp_ws* nom, const mpcqp_ws* rel, const mpcqp_fleet* f) 
 // enqueue one step (no validation)
 int enqueue_step(mpcqp_ws* nom, mpcqp_ws* rel, const mpcqp_fleet* f, hipStream_t s) {
   const int V = f->vehicles;
-  const int N = nom->p.horizon;
-  const mpcqp::launcher_t solve = mpcqp::launcher(N);
+  const mpcqp::launcher_t solve = mpcqp::launcher(nom->p);
+  if (mpcqp::launcher(rel->p) != solve) return fail(MPCQP_E_ARG, "nominal and relaxed workspaces differ in kernel");
   if (!solve) return fail(MPCQP_E_HORIZON, "horizon not compiled into this build");
   nom->built_B = -1;  // the fleet overwrites the models: a later mpcqp_solve needs its own build
   rel->built_B = -1;

@@ -34,7 +34,7 @@ STATUS_NAMES = {
 
 # OSQP settings used by the reference (src/control/mpc_controller.py:121-131) plus the
 # OSQP defaults it relies on implicitly.
-ABI_VERSION = 4  # MPCQP_ABI_VERSION (include/mpcqp.h)
+ABI_VERSION = 5  # MPCQP_ABI_VERSION (include/mpcqp.h)
 
 DEFAULT_SOLVER_SETTINGS = dict(
     rho=0.1,
@@ -54,6 +54,7 @@ DEFAULT_SOLVER_SETTINGS = dict(
     polish_from=150,
     polish_attempt_max_iter=30,
     polish_near=3.0,
+    reproducible=0,
 )
 
 
@@ -91,6 +92,7 @@ class MpcqpParams(ctypes.Structure):
         ("polish_from", ctypes.c_int32),
         ("polish_attempt_max_iter", ctypes.c_int32),
         ("polish_near", ctypes.c_double),
+        ("reproducible", ctypes.c_int32),
     ]
 
 
@@ -246,6 +248,7 @@ _SYMBOLS = {
     "mpcqp_model_stride": ([ctypes.c_int], ctypes.c_int),
     "mpcqp_state_buffer": ([ctypes.c_void_p], ctypes.c_void_p),
     "mpcqp_state_stride": ([ctypes.c_int], ctypes.c_int),
+    "mpcqp_ws_state_stride": ([ctypes.c_void_p], ctypes.c_int),
     "mpcqp_debug_wave_ops": ([ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p], ctypes.c_int),
     "mpcqp_debug_stamps": ([ctypes.c_void_p, ctypes.c_int], ctypes.c_int),
 }

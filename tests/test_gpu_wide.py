@@ -87,6 +87,30 @@ def test_long_horizons_bit_exact_with_c_restatement(cuda, N, settings):
     assert np.array_equal(out["active"], ref["active"])
 
 
+@pytest.mark.parametrize("N,config,settings", [(1, "config3", {}), (5, "config3", {}), (10, "config3", {}),
+                                               (15, "config3", {"polish_near": 0.0}), (20, "config3", {}),
+                                               (20, "config2", {}), (20, "config3", {"polish_from": 0, "polish_near": 0.0}),
+                                               (31, "config3", {})])
+def test_reproducible_mode_bit_exact_with_c_restatement(cuda, N, config, settings):
+    """mpcqp_params.reproducible = 1 at the short horizons too (the bench's N = 20 included): every
+    QP's solution, status and ADMM / polish / factorization / line-search counts identical to the C
+    restatement given the same model -- 100 % of QPs -- and the exact optimum as the fast kernel."""
+    import cpu_solver
+    from mpcqp import scenarios
+
+    batch = scenarios.config2(64, horizon=N) if config == "config2" else scenarios.config3(64, horizon=N, seed=800 + N)
+    params = _params(N)
+    out, model = _solve_with_model(params, batch.x0, batch.ref, batch.u_prev, reproducible=1, **settings)
+    ref = cpu_solver.cpu_solve_models(params, model, **settings)
+    assert np.array_equal(out["status"], ref["status"])
+    assert np.array_equal(out["iters"], ref["iters"]), np.argwhere((out["iters"] != ref["iters"]).any(axis=1))
+    assert np.array_equal(out["U"], ref["U"])
+    assert np.array_equal(out["X"], ref["X"])
+    assert np.array_equal(out["active"], ref["active"])
+    fast, _ = _solve_with_model(params, batch.x0, batch.ref, batch.u_prev, **settings)
+    assert np.array_equal(fast["active"], out["active"]) and _rel(fast["U"], out["U"]) <= REL_TOL
+
+
 def test_long_horizon_newton_and_max_iter(cuda):
     """Method newton and an ADMM capped below convergence: statuses and counts as the C code."""
     import cpu_solver
