@@ -28,12 +28,14 @@ __device__ __forceinline__ LaneModel build_lane(const mpcqp_params& p, int lane,
     pc = ddmod - dd;
     if (fabs(dd) < kPi) pc = 0.0;
   }
-  // cumsum in numpy's sequential order (bit-exact)
+  // cumsum in numpy's sequential order (bit-exact).  Every correction is +0.0 or nonzero (ddmod -
+  // dd of equal finite values is +0.0), so a window without a wrap sums to +0.0 throughout.
   double cs = 0.0, mine = 0.0;
-  for (int j = 1; j <= N; ++j) {
-    cs = cs + readlane(pc, j);
-    if (lane == j) mine = cs;
-  }
+  if (wave_any(pc != 0.0))
+    for (int j = 1; j <= N; ++j) {
+      cs = cs + readlane(pc, j);
+      if (lane == j) mine = cs;
+    }
   m.uyaw = lane == 0 ? ryaw : ryaw + mine;
   // linearisation point of step k: ref[max(k-1, 0)]
   const double psi_m1 = dpp<kWaveShr1>(m.uyaw);

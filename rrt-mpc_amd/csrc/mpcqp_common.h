@@ -129,15 +129,29 @@ __device__ __forceinline__ double rscan_max(double v, int lane) {
   if (row <= 0) off = fmax(off, t1);
   return fmax(v, off);
 }
+// max / min without LLVM's IEEE-mode operand canonicalization (it adds a v_max_f64 x, x, x for
+// every operand not known to be canonical -- DPP results, values kept opaque across solver
+// iterations).  No kernel here produces signalling NaNs, and on quiet operands the instruction
+// is IEEE maxNum / minNum, i.e. fmax / fmin bit for bit.
+__device__ __forceinline__ double max_nc(double a, double b) {
+  double r;
+  asm("v_max_f64 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+__device__ __forceinline__ double min_nc(double a, double b) {
+  double r;
+  asm("v_min_f64 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
 // wave-uniform sum / max: the inclusive scan's last lane
 __device__ __forceinline__ double wave_sum(double v) { return readlane(scan_add(v, 0), 63); }
 __device__ __forceinline__ double wave_max(double v) {  // v >= 0
-  v = fmax(v, dpp<kRowShr1>(v));
-  v = fmax(v, dpp<kRowShr2>(v));
-  v = fmax(v, dpp<kRowShr4>(v));
-  v = fmax(v, dpp<kRowShr8>(v));
-  v = fmax(v, dpp_rows<kRowBcast15, 0xa>(v));
-  v = fmax(v, dpp_rows<kRowBcast31, 0xc>(v));
+  v = max_nc(v, dpp<kRowShr1>(v));
+  v = max_nc(v, dpp<kRowShr2>(v));
+  v = max_nc(v, dpp<kRowShr4>(v));
+  v = max_nc(v, dpp<kRowShr8>(v));
+  v = max_nc(v, dpp_rows<kRowBcast15, 0xa>(v));
+  v = max_nc(v, dpp_rows<kRowBcast31, 0xc>(v));
   return readlane(v, 63);
 }
 // lane i <- lane i-2 (0 for i < 2);  lane i <- lane i+2 (0 past the wave)

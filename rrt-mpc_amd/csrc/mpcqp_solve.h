@@ -933,41 +933,53 @@ __device__ __forceinline__ int polish_qp(Ctx<N>& C, double& x, const double zg[3
 // OSQP's iteration on the scaled problem (rho / sigma / alpha / adaptive rho / termination as
 // the reference settings).  From iteration polish_from on, a termination check that fails also
 // attempts the polish: an exact optimum found there satisfies the termination test itself.
-// Returns the ADMM flag (-1 numerical error, 0 not converged, 1 converged, 2 solved by an early
-// polish, 3 max_iter reached within 10x the tolerances); x, z, the counters out.
+// The loop state lives in the caller (AdmmState): admm_run stops at such an attempt and the
+// caller resumes it after a failed one, so the kernel holds ONE inlined copy of the polish (the
+// early attempts, the final polish and method newton share the call site in k_solve) -- the
+// polish is a third of k_solve's code, which is larger than the 64 KB instruction cache.
+struct AdmmState {
+  double x, z[3], y[3], rho;
+  double rho_next;  // the adaptive-rho update of the check that stopped for an attempt
+  int it, nfact;
+  bool need_fact;   // form + sweep at the next entry (start, rho change, after a failed attempt)
+  bool rho_change;  // rho_next is pending (applied after a failed attempt)
+};
+enum : int { kAdmmBad = -1, kAdmmMaxIter = 0, kAdmmConverged = 1, kAdmmApprox = 3, kAdmmAttempt = 4 };
+
+// Runs ADMM until an event: kAdmmBad (numerical error), kAdmmConverged (eps_abs/eps_rel met),
+// kAdmmAttempt (a check asks for an early polish; rho_change/rho_next hold that check's
+// adaptive-rho decision), kAdmmApprox / kAdmmMaxIter (max_iter reached within / outside 10x the
+// tolerances: OSQP's solved_inaccurate / max_iter_reached).
 template <int N>
-__device__ __forceinline__ int admm_qp(const mpcqp_params& p, Ctx<N>& C, bool bad, double& x_out, double z_out[3],
-                                       int& it_out, int& nfact_out, int& pol_it, int& n_ls, double* __restrict__ dbg) {
+__device__ __forceinline__ int admm_run(const mpcqp_params& p, Ctx<N>& C, AdmmState& S) {
   const bool act = C.act;
-  double x = 0.0, z[3] = {0.0, 0.0, 0.0}, y[3] = {0.0, 0.0, 0.0};
-  double rho = p.rho;
   const double sg = p.sigma, alpha = p.alpha;
-  bool ok = false, polished = false, approx = false;
-  int it = 0, nfact = 0;
   const bool early = p.polish != 0 && p.polish_from > 0;
-  Stamps T, T2;
-  T2.begin();
-  while (it < p.max_iter && !bad && !ok && !polished) {
-    {
-      const double rw[3] = {rho, rho, rho};
+  int ev = kAdmmMaxIter;
+  bool done = false;
+  Stamps T;
+  while (S.it < p.max_iter && !done) {
+    if (S.need_fact) {
+      const double rw[3] = {S.rho, S.rho, S.rho};
       T.begin();
       C.form(sg, rw);
       T.end(0);
-      ++nfact;
+      ++S.nfact;
       T.begin();
       const bool okf = C.sweep();
       T.end(1);
       if (wave_any(!okf)) {
-        bad = true;
+        ev = kAdmmBad;
         break;
       }
+      S.need_fact = false;
     }
-    bool refactor = false;
     // The z-update is the prox of the eliminated slack's penalty w dist(z, [lo, hi])^2:
     //   zn = vv - pb (vv - clamp(vv, lo, hi)),  pb = 2w / (rho + 2w)
     // (= (rho vv + 2 w bnd) / (rho + 2 w) outside the bounds, vv inside), and the dual update
     // y + rho (v - zn) with vv = v + y / rho is exactly rho pb (vv - clamp): no selects, and no
     // cancellation of y against rho (v - zn).
+    const double rho = S.rho;
     double pb[3], rpb[3];
 #pragma unroll
     for (int r = 0; r < 3; ++r) {
@@ -975,26 +987,26 @@ __device__ __forceinline__ int admm_qp(const mpcqp_params& p, Ctx<N>& C, bool ba
       rpb[r] = rho * pb[r];
     }
     const double ir = 1.0 / rho, oma = 1.0 - alpha;
-    while (!refactor && it < p.max_iter) {
-      ++it;
+    while (!S.need_fact && S.it < p.max_iter) {
+      const int it = ++S.it;
       C.opaque();
       T.begin();
       double tmp[3];
 #pragma unroll
-      for (int r = 0; r < 3; ++r) tmp[r] = rho * z[r] - y[r];
-      const double rhs = C.CTmul(tmp) + sg * x - C.qv;
+      for (int r = 0; r < 3; ++r) tmp[r] = rho * S.z[r] - S.y[r];
+      const double rhs = C.CTmul(tmp) + sg * S.x - C.qv;
       // relaxation folded into the step: xa = alpha xt, Cbar xa = alpha Cbar xt
       const double xa = alpha * C.inv_mul(rhs);
       double za[3];
       C.Cmul(xa, za);
-      x = xa + oma * x;
+      S.x = xa + oma * S.x;
 #pragma unroll
       for (int r = 0; r < 3; ++r) {
-        const double v = za[r] + oma * z[r];
-        const double vv = v + y[r] * ir;
-        const double d = vv - fmin(fmax(vv, C.lo[r]), C.hi[r]);
-        z[r] = vv - pb[r] * d;
-        y[r] = rpb[r] * d;
+        const double v = za[r] + oma * S.z[r];
+        const double vv = v + S.y[r] * ir;
+        const double d = vv - min_nc(max_nc(vv, C.lo[r]), C.hi[r]);
+        S.z[r] = vv - pb[r] * d;
+        S.y[r] = rpb[r] * d;
       }
       T.end(2);
       if (it % p.check_termination == 0 || it == p.max_iter) {
@@ -1002,6 +1014,7 @@ __device__ __forceinline__ int admm_qp(const mpcqp_params& p, Ctx<N>& C, bool ba
         // Residual norms (OSQP: unscaled for termination, scaled for the rho update).  The
         // lane maxima are combined before the wave reductions (max distributes), which keeps
         // the check's live set small.
+        const double x = S.x;
         double Ax[3];
         C.Cmul(x, Ax);
         double pr = 0, nprim = 0, spr = 0, snprim = 0;
@@ -1009,10 +1022,10 @@ __device__ __forceinline__ int admm_qp(const mpcqp_params& p, Ctx<N>& C, bool ba
         for (int r = 0; r < 3; ++r) {
           if (C.E[r] > 0.0) {
             const double ie = 1.0 / C.E[r];
-            pr = fmax(pr, fabs((Ax[r] - z[r]) * ie));
-            nprim = fmax(nprim, fmax(fabs(Ax[r] * ie), fabs(z[r] * ie)));
-            spr = fmax(spr, fabs(Ax[r] - z[r]));
-            snprim = fmax(snprim, fmax(fabs(Ax[r]), fabs(z[r])));
+            pr = fmax(pr, fabs((Ax[r] - S.z[r]) * ie));
+            nprim = fmax(nprim, fmax(fabs(Ax[r] * ie), fabs(S.z[r] * ie)));
+            spr = fmax(spr, fabs(Ax[r] - S.z[r]));
+            snprim = fmax(snprim, fmax(fabs(Ax[r]), fabs(S.z[r])));
           }
         }
         pr = wave_max(pr);
@@ -1020,7 +1033,7 @@ __device__ __forceinline__ int admm_qp(const mpcqp_params& p, Ctx<N>& C, bool ba
         spr = wave_max(spr);
         snprim = wave_max(snprim);
         const double Px = C.Pmul(x);
-        const double Aty = C.CTmul(y);
+        const double Aty = C.CTmul(S.y);
         double du = 0, ndual = 0, sdu = 0, sndual = 0;
         if (act) {
           const double id = 1.0 / C.D;
@@ -1040,109 +1053,86 @@ __device__ __forceinline__ int admm_qp(const mpcqp_params& p, Ctx<N>& C, bool ba
         const double ed = p.eps_abs + p.eps_rel * ndual * ic;
         T.end(3);
         // fmax drops NaNs, so test the iterate itself
-        if (wave_any(!isfinite(x) || !isfinite(z[0] + z[1] + z[2]) || !isfinite(y[0] + y[1] + y[2])) ||
+        if (wave_any(!isfinite(x) || !isfinite(S.z[0] + S.z[1] + S.z[2]) || !isfinite(S.y[0] + S.y[1] + S.y[2])) ||
             !isfinite(pr) || !isfinite(du)) {
-          bad = true;
+          ev = kAdmmBad;
+          done = true;
           break;
         }
         if (pr <= ep && du <= ed) {
-          ok = true;
+          ev = kAdmmConverged;
+          done = true;
           break;
         }
         // OSQP at max_iter: the same test with eps_abs and eps_rel x10 passes -> solved_inaccurate
-        // (no polish); otherwise max_iter_reached
-        // (the loop ends by itself after this check)
-        approx = it == p.max_iter && pr <= 10.0 * p.eps_abs + 10.0 * p.eps_rel * nprim &&
-                 du <= 10.0 * p.eps_abs + 10.0 * p.eps_rel * ndual * ic;
-        // ... from polish_from on, or earlier once both residuals are near their tolerances
-        const bool near = p.polish_near > 0.0 && it >= 2 * p.check_termination &&
-                          fmax(pr / ep, du / ed) < p.polish_near;
-        if (early && (it >= p.polish_from || near) && it < p.max_iter) {
-          double xp = x;
-          const int pr_ = polish_qp<N>(C, xp, z, p.polish_attempt_max_iter, pol_it, nfact, n_ls);
-          if (pr_ < 0) {
-            bad = true;
-            break;
-          }
-          if (pr_ > 0) {
-            x = xp;
-            polished = true;
-            break;
-          }
-          refactor = true;  // the attempt used the inverse's registers
-        }
+        // (no polish); otherwise max_iter_reached (the loop ends by itself after this check)
+        if (it == p.max_iter && pr <= 10.0 * p.eps_abs + 10.0 * p.eps_rel * nprim &&
+            du <= 10.0 * p.eps_abs + 10.0 * p.eps_rel * ndual * ic)
+          ev = kAdmmApprox;
+        // this check's adaptive-rho decision (a function of its residuals alone)
+        bool rc = false;
+        double rn = rho;
         if (p.adaptive_rho && it % p.adaptive_rho_interval == 0) {
           const double pn = spr / (snprim + kDivTol);
           const double dn = sdu / (sndual + kDivTol);
-          double rn = rho * sqrt(pn / (dn + kDivTol));
+          rn = rho * sqrt(pn / (dn + kDivTol));
           rn = fmin(fmax(rn, kRhoMin), kRhoMax);
-          if (rn > rho * p.adaptive_rho_tolerance || rn < rho / p.adaptive_rho_tolerance) {
-            rho = rn;
-            refactor = true;
-          }
+          rc = rn > rho * p.adaptive_rho_tolerance || rn < rho / p.adaptive_rho_tolerance;
+        }
+        // early polish from polish_from on, or earlier once both residuals are near their
+        // tolerances: the caller polishes, then resumes with this rho decision if it failed
+        const bool near = p.polish_near > 0.0 && it >= 2 * p.check_termination &&
+                          fmax(pr / ep, du / ed) < p.polish_near;
+        if (early && (it >= p.polish_from || near) && it < p.max_iter) {
+          S.rho_change = rc;
+          S.rho_next = rn;
+          ev = kAdmmAttempt;
+          done = true;
+          break;
+        }
+        if (rc) {
+          S.rho = rn;
+          S.need_fact = true;
         }
       }
     }
   }
-  const int flag = bad ? -1 : (polished ? 2 : (ok ? 1 : (approx ? 3 : 0)));
-  if (dbg) {
-    dbg[state_lane_off(N) + kFx * kWave + threadIdx.x] = act ? x : 0.0;
-    if (threadIdx.x == 0) {
-      double* sc = dbg + state_scal_off(N);
-      sc[1] = flag < 0 ? -1.0 : (flag > 0 ? 1.0 : 0.0);
-      sc[2] = (double)it;
-      sc[3] = (double)nfact;
-    }
-  }
-  x_out = act ? x : 0.0;
-#pragma unroll
-  for (int r = 0; r < 3; ++r) z_out[r] = z[r];
-  it_out = it;
-  nfact_out = nfact;
-  T2.end(0);
-  T.flush(0);   // g_stamps[0..3]: form, sweep, ADMM iteration body, termination checks
-  T2.flush(4);  // g_stamps[4]: whole ADMM phase
-  return flag;
+  T.flush(0);  // g_stamps[0..3]: form, sweep, ADMM iteration body, termination checks
+  return ev;
 }
 
-// ------------------------------------------------------------------ K2c: polish + outputs
+// The ADMM phase's solver state for debug_state (x, flag, iterations, factorizations).
+template <int N>
+__device__ __forceinline__ void admm_debug_state(double* __restrict__ dbg, bool act, double x, int flag, int it,
+                                                 int nfact) {
+  if (!dbg) return;
+  dbg[state_lane_off(N) + kFx * kWave + threadIdx.x] = act ? x : 0.0;
+  if (threadIdx.x == 0) {
+    double* sc = dbg + state_scal_off(N);
+    sc[1] = flag < 0 ? -1.0 : (flag > 0 ? 1.0 : 0.0);
+    sc[2] = (double)it;
+    sc[3] = (double)nfact;
+  }
+}
+
+// ------------------------------------------------------------------ K2c: status + outputs
+// x: the returned iterate (the polish's last iterate when the final polish ran), x_admm: the
+// ADMM iterate (returned when that polish did not converge, as OSQP does).
 template <int N>
 __device__ __forceinline__ void finish_qp(const mpcqp_params& p, int b, const double* __restrict__ model,
                                           const double* __restrict__ in_x0, const double* __restrict__ in_ref,
                                           const double* __restrict__ in_up, const double* kept_model, Ctx<N>& C,
-                                          double x_in, const double z_admm[3], int admm_flag, int admm_it, int nfact,
-                                          int pol_it, int n_ls, double* __restrict__ u0o, double* __restrict__ Xo,
-                                          double* __restrict__ Uo, int32_t* __restrict__ statuso,
-                                          int32_t* __restrict__ iterso, uint8_t* __restrict__ activeo) {
+                                          double x, double x_admm, int admm_flag, bool do_polish, bool pol_ok,
+                                          bool bad, int admm_it, int nfact, int pol_it, int n_ls,
+                                          double* __restrict__ u0o, double* __restrict__ Xo, double* __restrict__ Uo,
+                                          int32_t* __restrict__ statuso, int32_t* __restrict__ iterso,
+                                          uint8_t* __restrict__ activeo) {
   constexpr int n = 2 * N;
   const int lane = threadIdx.x;
   const bool act = C.act;
   const bool use_admm = p.method == MPCQP_METHOD_ADMM;
-  const bool polished = admm_flag == 2;  // exact optimum already found by an early polish
-  const bool approx = admm_flag == 3;    // OSQP's solved_inaccurate at max_iter: not polished
-  // OSQP polishes only a solved ADMM run (status solved); method newton is the polish alone
-  const bool do_polish = use_admm ? (p.polish != 0 && admm_flag == 1) : true;
-  bool bad = admm_flag < 0;  // non-finite data (setup) or ADMM numerical error
-  const bool admm_ok = admm_flag == 1;
-  double x = use_admm ? x_in : 0.0;
-  const double x_admm = x;
-  bool pol_ok = polished;
-  Stamps T2;
-  T2.begin();
-  if (do_polish && !bad) {
-    double zg[3];
-    if (use_admm) {  // first guess: the ADMM z iterate (the prox output)
-#pragma unroll
-      for (int r = 0; r < 3; ++r) zg[r] = z_admm[r];
-    } else {
-      C.Cmul(x, zg);
-    }
-    const int r_ = polish_qp<N>(C, x, zg, p.polish_max_iter, pol_it, nfact, n_ls);
-    if (r_ < 0) bad = true;
-    pol_ok = r_ > 0;
-  }
-  T2.end(0);
-  T2.flush(12);  // g_stamps[12]: polish phase of k_finish
+  const bool approx = admm_flag == kAdmmApprox;  // OSQP's solved_inaccurate at max_iter: not polished
+  const bool admm_ok = admm_flag == kAdmmConverged;
   Stamps T3;
   T3.begin();
   if (wave_any(!isfinite(x))) bad = true;
@@ -1306,12 +1296,76 @@ __global__ __launch_bounds__(kWave, kSolveWavesPerEU<N>) void k_solve(mpcqp_para
   Stamps TK;
   TK.begin();
   Ctx<N> C;
-  const bool bad = setup_qp<N>(p, b, model, in_x0, in_ref, in_up, C, sm, state + (size_t)b * state_stride(N), dbg);
-  double x = 0.0, z[3] = {0.0, 0.0, 0.0};
-  int flag = bad ? -1 : 0, it = 0, nfact = 0, pol_it = 0, n_ls = 0;
-  if (p.method == MPCQP_METHOD_ADMM) flag = admm_qp<N>(p, C, bad, x, z, it, nfact, pol_it, n_ls, dbg);
-  finish_qp<N>(p, b, model, in_x0, in_ref, in_up, sm.model, C, x, z, flag, it, nfact, pol_it, n_ls, u0o, Xo, Uo, statuso, iterso,
-               activeo);
+  bool bad = setup_qp<N>(p, b, model, in_x0, in_ref, in_up, C, sm, state + (size_t)b * state_stride(N), dbg);
+  const bool use_admm = p.method == MPCQP_METHOD_ADMM;
+  AdmmState S;
+  S.x = 0.0;
+#pragma unroll
+  for (int r = 0; r < 3; ++r) S.z[r] = S.y[r] = 0.0;
+  S.rho = S.rho_next = p.rho;
+  S.it = 0;
+  S.nfact = 0;
+  S.need_fact = true;
+  S.rho_change = false;
+  int flag = bad ? kAdmmBad : kAdmmMaxIter, pol_it = 0, n_ls = 0;
+  double x = 0.0, x_admm = 0.0;
+  bool do_polish = false, pol_ok = false;
+  if (use_admm && bad) admm_debug_state<N>(dbg, C.act, 0.0, flag, 0, 0);
+  // ADMM with its early polish attempts, then the final polish: ONE polish call site
+  while (!bad) {
+    // kind 1: early attempt (ADMM resumes if it fails), 2: final polish (OSQP polishes only a
+    // solved ADMM run; method newton is the polish alone, from x = 0)
+    int kind = 0;
+    double zg[3];
+    if (use_admm) {
+      const int ev = admm_run<N>(p, C, S);
+      if (ev == kAdmmAttempt) {
+        kind = 1;
+      } else {
+        flag = ev;
+        x = x_admm = C.act ? S.x : 0.0;
+        admm_debug_state<N>(dbg, C.act, x, flag, S.it, S.nfact);
+        do_polish = p.polish != 0 && flag == kAdmmConverged;
+        kind = do_polish ? 2 : 0;
+        bad = flag == kAdmmBad;
+      }
+#pragma unroll
+      for (int r = 0; r < 3; ++r) zg[r] = S.z[r];  // first active-set guess: the ADMM z iterate
+    } else {
+      do_polish = true;
+      kind = 2;
+      C.Cmul(x, zg);
+    }
+    if (kind == 0) break;
+    double xp = kind == 1 ? S.x : x;
+    Stamps T2;
+    T2.begin();
+    const int r_ = polish_qp<N>(C, xp, zg, kind == 1 ? p.polish_attempt_max_iter : p.polish_max_iter, pol_it,
+                                S.nfact, n_ls);
+    T2.end(0);
+    T2.flush(12);  // g_stamps[12]: polish
+    if (kind == 2) {  // final polish: its iterate is returned when it converged
+      x = xp;
+      bad = r_ < 0;
+      pol_ok = r_ > 0;
+      break;
+    }
+    if (r_ != 0) {  // the attempt reached the exact optimum (ADMM flag 2) or failed numerically
+      flag = r_ > 0 ? 2 : kAdmmBad;
+      bad = r_ < 0;
+      pol_ok = r_ > 0;
+      x = x_admm = C.act ? (pol_ok ? xp : S.x) : 0.0;
+      admm_debug_state<N>(dbg, C.act, x, flag, S.it, S.nfact);
+      break;
+    }
+    // a failed attempt resumes ADMM: refactor (the attempt used the inverse's registers) with
+    // the rho of that check's adaptive update
+    S.need_fact = true;
+    if (S.rho_change) S.rho = S.rho_next;
+    S.rho_change = false;
+  }
+  finish_qp<N>(p, b, model, in_x0, in_ref, in_up, sm.model, C, x, x_admm, flag, do_polish, pol_ok, bad, S.it, S.nfact,
+               pol_it, n_ls, u0o, Xo, Uo, statuso, iterso, activeo);
   TK.end(0);
   TK.flush(22);  // g_stamps[22]: the whole QP
   if (dbg && threadIdx.x == 0) {  // this wave's cycles, start to finish, and its work (tools/qp_cycles.py)
