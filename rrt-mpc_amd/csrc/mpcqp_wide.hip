@@ -119,6 +119,17 @@ struct Blk {
     __syncthreads();
     return r;
   }
+  // sum in tree order (the fast mode's line search; the reproducible mode sums in the C order)
+  __device__ double sum(double v) const {
+    for (int o = kWave / 2; o > 0; o >>= 1) v += __shfl_xor(v, o, kWave);
+    __syncthreads();
+    if ((threadIdx.x & (kWave - 1)) == 0) red[threadIdx.x / kWave] = v;
+    __syncthreads();
+    double r = red[0];
+    for (int k = 1; k < kTW; ++k) r += red[k];
+    __syncthreads();
+    return r;
+  }
   // thread 0's value to every thread
   __device__ double bcast0(double v) const {
     __syncthreads();
@@ -370,6 +381,48 @@ struct Wide {
     return sweep();
   }
   __device__ static int code(double z, double l, double u) { return z > u ? 2 : (z < l ? 1 : 0); }
+  // Fast mode's polish: Sherman-Morrison on K = A^{-1} for A' = A + delta c c', c the scaled row r
+  // of Cbar (at most three entries: Cmul's coefficients).  K' = K - kap u u', u = K c (three
+  // columns of K), kap = delta / (1 + delta c'u).  false (K untouched) when the denominator is not
+  // safely positive -- the caller refactorizes.
+  __device__ bool rank1(int r, double delta) const {
+    const int N = L.N, n = L.n;
+    const double* D = at(L.oD);
+    const double* E = at(L.oEr);
+    const double* k1 = at(L.oK1);
+    const double* k2 = at(L.oK2);
+    int idx[3] = {0, 0, 0};
+    double cf[3] = {0.0, 0.0, 0.0};
+    if (r < N) {
+      idx[0] = 2 * r;
+      cf[0] = E[r] * D[2 * r];
+    } else if (r < 3 * N) {
+      const int p = r - N;
+      for (int a = 0; a < 2; ++a)
+        if (p - 2 * a >= 0) {
+          idx[a] = p - 2 * a;
+          cf[a] = (E[r] * k1[2 * p + a]) * D[p - 2 * a];
+        }
+    } else {
+      const int p = r - 3 * N;
+      for (int a = 0; a < 3; ++a)
+        if (p - 2 * a >= 0) {
+          idx[a] = p - 2 * a;
+          cf[a] = (E[r] * k2[3 * p + a]) * D[p - 2 * a];
+        }
+    }
+    double* uv = at(L.oCm);
+    __syncthreads();
+    for (int i = tid; i < n; i += kT) uv[i] = (cf[0] * K(i, idx[0]) + cf[1] * K(i, idx[1])) + cf[2] * K(i, idx[2]);
+    __syncthreads();
+    const double cu = (cf[0] * uv[idx[0]] + cf[1] * uv[idx[1]]) + cf[2] * uv[idx[2]];
+    const double den = 1.0 + delta * cu;
+    if (!(den > kRank1Min) || !isfinite(den)) return false;  // uniform: every thread, same values
+    const double kap = delta / den;
+    for_ij(n, tid, [&](int i, int j, int) { K(i, j) -= (kap * uv[i]) * uv[j]; });
+    __syncthreads();
+    return true;
+  }
 };
 
 // condensing + scaling (mpcqp_cpu.c condense + setup_qp); returns bad (non-finite data)
@@ -612,6 +665,11 @@ __device__ bool wide_setup(const mpcqp_params& p, Wide& S) {
 }
 
 // mpcqp_cpu.c polish_run: 1 exact optimum found (x = it), 0 not within max_it passes, -1 failure
+// FAST (reproducible = 0, N >= MPCQP_WIDE_MIN_HORIZON): passes after the first update the
+// inverse by rank-1 changes of the rows that entered or left the set (a full form + sweep when
+// more than n/2 changed or an update is unsafe), and the line search's sums run in tree order --
+// the one-wave kernel's polish.  Otherwise every pass refactorizes and sums run in the C order.
+template <bool FAST>
 __device__ int wide_polish(Wide& S, double* x, const double* zg, int max_it, int& pol_it, int& n_fact, int& n_ls) {
 #pragma clang fp contract(off)
   const WideLayout& L = S.L;
@@ -635,6 +693,9 @@ __device__ int wide_polish(Wide& S, double* x, const double* zg, int max_it, int
   double* zd = S.at(L.oZd);
   double* t1 = S.at(L.oT1);
   double* t2 = S.at(L.oT2);
+  double* rwf = S.at(L.oEl);  // FAST: soft-row weights of the current factorization (setup scratch)
+  double* chg = S.at(L.oT1);  // FAST: rows whose weight changed (the line search's scratch otherwise)
+  bool have_fact = false;
   S.Cmul(x, zc);
   S.matvec(S.P, L.ps, x, Px);
   for (int r = tid; r < m; r += kT) cd[r] = Wide::code(zg[r], l[r], u[r]);
@@ -647,7 +708,28 @@ __device__ int wide_polish(Wide& S, double* x, const double* zg, int max_it, int
     }
     S.mark();
     ++n_fact;
-    if (!S.form_inverse(0.0, rw)) return -1;
+    bool refac = true;
+    if (FAST && have_fact) {
+      __syncthreads();
+      int nchg = 0;
+      if (tid == 0)
+        for (int r = 0; r < m; ++r)
+          if (rw[r] != rwf[r]) chg[nchg++] = (double)r;
+      nchg = (int)S.blk.bcast0((double)nchg);
+      refac = nchg > n / 2;
+      for (int k = 0; k < nchg && !refac; ++k) {
+        const int r = (int)chg[k];
+        refac = !S.rank1(r, rw[r] - rwf[r]);
+      }
+    }
+    if (refac) {
+      if (!S.form_inverse(0.0, rw)) return -1;
+      have_fact = true;
+    }
+    if (FAST) {
+      for (int r = tid; r < m; r += kT) rwf[r] = rw[r];
+      __syncthreads();
+    }
     S.stamp(5);
     S.CTmul(tmp, rhs);
     for (int i = tid; i < n; i += kT) rhs[i] -= q[i];
@@ -686,29 +768,51 @@ __device__ int wide_polish(Wide& S, double* x, const double* zg, int max_it, int
     }
     for (int r = tid; r < m; r += kT) zd[r] = zn[r] - zc[r];
     __syncthreads();
-    double qd = 0.0, lin = 0.0;  // every thread, the C code's order
+    double qd = 0.0, lin = 0.0;
+    if constexpr (FAST) {
+      double a = 0.0, c = 0.0;
+      for (int i = tid; i < n; i += kT) {
+        a += dx[i] * Pd[i];
+        c += (Px[i] + q[i]) * dx[i];
+      }
+      qd = S.blk.sum(a);
+      lin = S.blk.sum(c);
+    } else {
 #pragma unroll 8
-    for (int i = 0; i < n; ++i) {
-      qd += dx[i] * Pd[i];
-      lin += (Px[i] + q[i]) * dx[i];
+      for (int i = 0; i < n; ++i) {  // every thread, the C code's order
+        qd += dx[i] * Pd[i];
+        lin += (Px[i] + q[i]) * dx[i];
+      }
     }
     double t = 1.0;
     for (int ls = 0; ls < 40; ++ls) {
       ++n_ls;
-      for (int r = tid; r < m; r += kT) {
-        const double zt = zc[r] + t * zd[r];
-        const double rr = zt > u[r] ? zt - u[r] : (zt < l[r] ? zt - l[r] : 0.0);
-        t1[r] = 2.0 * w[r] * rr * zd[r];
-        t2[r] = rr != 0.0 ? 2.0 * w[r] * zd[r] * zd[r] : -1.0;  // -1: not added (the term is >= 0)
-      }
-      __syncthreads();
       double d1 = lin + t * qd, d2 = qd;
+      if constexpr (FAST) {
+        double a = 0.0, c = 0.0;
+        for (int r = tid; r < m; r += kT) {
+          const double zt = zc[r] + t * zd[r];
+          const double rr = zt > u[r] ? zt - u[r] : (zt < l[r] ? zt - l[r] : 0.0);
+          a += 2.0 * w[r] * rr * zd[r];
+          if (rr != 0.0) c += 2.0 * w[r] * zd[r] * zd[r];
+        }
+        d1 += S.blk.sum(a);
+        d2 += S.blk.sum(c);
+      } else {
+        for (int r = tid; r < m; r += kT) {
+          const double zt = zc[r] + t * zd[r];
+          const double rr = zt > u[r] ? zt - u[r] : (zt < l[r] ? zt - l[r] : 0.0);
+          t1[r] = 2.0 * w[r] * rr * zd[r];
+          t2[r] = rr != 0.0 ? 2.0 * w[r] * zd[r] * zd[r] : -1.0;  // -1: not added (the term is >= 0)
+        }
+        __syncthreads();
 #pragma unroll 8
-      for (int r = 0; r < m; ++r) {  // the C code's order; d2 takes the rows with rr != 0 only
-        d1 += t1[r];
-        if (t2[r] >= 0.0) d2 += t2[r];
+        for (int r = 0; r < m; ++r) {  // the C code's order; d2 takes the rows with rr != 0 only
+          d1 += t1[r];
+          if (t2[r] >= 0.0) d2 += t2[r];
+        }
+        __syncthreads();
       }
-      __syncthreads();
       if (d1 <= 0.0 || !(d2 > 0.0)) break;
       const double tn = fmax(0.0, t - d1 / d2);
       if (tn >= t) break;
@@ -733,6 +837,7 @@ __device__ int wide_polish(Wide& S, double* x, const double* zg, int max_it, int
 }
 
 // mpcqp_cpu.c mpcqp_cpu_solve_one after setup: ADMM (+ early polish), final polish, outputs
+template <bool FAST>
 __device__ void wide_solve(const mpcqp_params& p, Wide& S, bool bad, int b, double* __restrict__ u0o,
                            double* __restrict__ Xo, double* __restrict__ Uo, int32_t* __restrict__ statuso,
                            int32_t* __restrict__ iterso, uint8_t* __restrict__ activeo) {
@@ -869,7 +974,7 @@ __device__ void wide_solve(const mpcqp_params& p, Wide& S, bool bad, int b, doub
         if (p.polish && p.polish_from > 0 && (it >= p.polish_from || near) && it < p.max_iter) {
           for (int i = tid; i < n; i += kT) xp[i] = x[i];
           __syncthreads();
-          const int pr_ = wide_polish(S, xp, z, p.polish_attempt_max_iter, pol_it, n_fact, n_ls);
+          const int pr_ = wide_polish<FAST>(S, xp, z, p.polish_attempt_max_iter, pol_it, n_fact, n_ls);
           if (pr_ < 0) {
             bad = true;
             break;
@@ -909,7 +1014,7 @@ __device__ void wide_solve(const mpcqp_params& p, Wide& S, bool bad, int b, doub
       zg = zt;
     }
     (void)zc;
-    const int r_ = wide_polish(S, x, zg, p.polish_max_iter, pol_it, n_fact, n_ls);
+    const int r_ = wide_polish<FAST>(S, x, zg, p.polish_max_iter, pol_it, n_fact, n_ls);
     if (r_ < 0) {
       bad = true;
     } else if (r_ > 0) {
@@ -996,7 +1101,7 @@ __device__ void wide_solve(const mpcqp_params& p, Wide& S, bool bad, int b, doub
 // workspace, 0 both in the workspace.  A compile-time choice, so every access is a ds_* or a
 // global_* instruction (a pointer that may be either compiles to flat accesses, which wait for
 // all outstanding memory operations: ~100x slower here).
-template <int kMode>
+template <int kMode, bool FAST>
 __global__ __launch_bounds__(kT) void k_solve_wide(mpcqp_params p, int B, const uint8_t* __restrict__ mask,
                                                    const double* __restrict__ model, double* __restrict__ wide,
                                                    double* __restrict__ u0o, double* __restrict__ Xo,
@@ -1037,7 +1142,7 @@ __global__ __launch_bounds__(kT) void k_solve_wide(mpcqp_params p, int B, const 
   S.mark();
   const bool bad = wide_setup(p, S);
   S.stamp(0);
-  wide_solve(p, S, bad, b, u0o, Xo, Uo, statuso, iterso, activeo);
+  wide_solve<FAST>(p, S, bad, b, u0o, Xo, Uo, statuso, iterso, activeo);
 }
 
 }  // namespace
@@ -1057,11 +1162,13 @@ void launch_solve_wide(hipStream_t s, const Launch& L) {
     hipLaunchKernelGGL(kern, dim3(L.B), dim3(kT), lds, s, *L.p, L.B, L.mask, L.model, wide, L.u0, L.X, L.U, L.st,
                        L.it, L.ac);
   };
+  // reproducible = 1: the C restatement op for op; 0 (N >= MPCQP_WIDE_MIN_HORIZON): the fast polish
+  const bool fast = L.p->reproducible == 0;
   if (arena + pbar <= kLds)
-    go(&k_solve_wide<2>, arena + pbar);
+    fast ? go(&k_solve_wide<2, true>, arena + pbar) : go(&k_solve_wide<2, false>, arena + pbar);
   else if (arena <= kLds)
-    go(&k_solve_wide<1>, arena);
+    fast ? go(&k_solve_wide<1, true>, arena) : go(&k_solve_wide<1, false>, arena);
   else
-    go(&k_solve_wide<0>, 0);
+    fast ? go(&k_solve_wide<0, true>, 0) : go(&k_solve_wide<0, false>, 0);
 }
 }  // namespace mpcqp

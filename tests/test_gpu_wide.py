@@ -2,11 +2,14 @@
 
 The reference builds its QP for any horizon (src/control/mpc_controller.py:47-57).  Horizons
 32..63 run one 256-thread workgroup per QP (the arena in LDS up to N ~ 48, in the workspace
-beyond).  Checks:
+beyond).  Two modes: reproducible = 1 is the C restatement parallelised without changing a
+floating-point operation; the default (fast) mode's polish updates the inverse by rank-1 changes
+and sums its line search in tree order.  Checks:
   * the exact oracle (mpc_oracle.solve_exact): U / X / u0 to 1e-8 relative, identical active sets;
-  * the C restatement fed the GPU's own LTV model (K1 output): U, X, statuses AND iteration
-    counts identical bit for bit -- the kernel is the C code parallelised without changing a
-    floating-point operation;
+  * reproducible = 1 against the C restatement fed the GPU's own LTV model (K1 output): U, X,
+    statuses AND iteration counts identical bit for bit;
+  * the fast mode against the same: statuses and active sets identical, U to 1e-8, ADMM
+    iterations identical and all four counters on >= 95 % of QPs;
   * the drop-in surface: MPCController(MPCConfig(horizon=40)) and a fleet at N = 40.
 """
 from __future__ import annotations
@@ -78,13 +81,32 @@ def test_long_horizons_bit_exact_with_c_restatement(cuda, N, settings):
 
     batch = scenarios.config3(48, horizon=N, seed=700 + N)
     params = _params(N)
-    out, model = _solve_with_model(params, batch.x0, batch.ref, batch.u_prev, **settings)
+    out, model = _solve_with_model(params, batch.x0, batch.ref, batch.u_prev, reproducible=1, **settings)
     ref = cpu_solver.cpu_solve_models(params, model, **settings)
     assert np.array_equal(out["status"], ref["status"])
     assert np.array_equal(out["iters"], ref["iters"]), np.argwhere((out["iters"] != ref["iters"]).any(axis=1))
     assert np.array_equal(out["U"], ref["U"])
     assert np.array_equal(out["X"], ref["X"])
     assert np.array_equal(out["active"], ref["active"])
+
+
+@pytest.mark.parametrize("N,settings", [(32, {}), (40, {}), (48, {"polish_from": 0, "polish_near": 0.0}), (63, {})])
+def test_long_horizons_fast_mode_against_c_restatement(cuda, N, settings):
+    """The default (fast) long-horizon mode: the same optimum and statuses as the C restatement,
+    the same ADMM run (its arithmetic is unchanged), rank-1 polish counters on >= 95 % of QPs."""
+    import cpu_solver
+    from mpcqp import scenarios
+
+    batch = scenarios.config3(64, horizon=N, seed=900 + N)
+    params = _params(N)
+    out, model = _solve_with_model(params, batch.x0, batch.ref, batch.u_prev, **settings)
+    ref = cpu_solver.cpu_solve_models(params, model, **settings)
+    assert np.array_equal(out["status"], ref["status"])
+    assert np.array_equal(out["active"], ref["active"])
+    assert _rel(out["U"], ref["U"]) <= REL_TOL and _rel(out["X"], ref["X"]) <= REL_TOL
+    same = (out["iters"] == ref["iters"]).all(axis=1).mean()
+    assert same >= 0.95, same
+    assert (out["iters"][:, 0] == ref["iters"][:, 0]).mean() >= 0.95
 
 
 @pytest.mark.parametrize("N,config,settings", [(1, "config3", {}), (5, "config3", {}), (10, "config3", {}),
@@ -120,11 +142,15 @@ def test_long_horizon_newton_and_max_iter(cuda):
     batch = scenarios.config3(32, horizon=N, seed=9)
     params = _params(N)
     for method, settings in (("newton", {}), ("admm", dict(max_iter=40, polish_from=0, polish_near=0.0))):
-        out, model = _solve_with_model(params, batch.x0, batch.ref, batch.u_prev, method=method, **settings)
+        out, model = _solve_with_model(params, batch.x0, batch.ref, batch.u_prev, method=method, reproducible=1,
+                                       **settings)
         ref = cpu_solver.cpu_solve_models(params, model, method=1 if method == "newton" else 0, **settings)
         assert np.array_equal(out["status"], ref["status"]), method
         assert np.array_equal(out["iters"], ref["iters"]), method
         assert np.array_equal(out["U"], ref["U"]), method
+        fast, _ = _solve_with_model(params, batch.x0, batch.ref, batch.u_prev, method=method, **settings)
+        assert np.array_equal(fast["status"], ref["status"]), method
+        assert _rel(fast["U"], ref["U"]) <= REL_TOL, method
 
 
 def test_mpc_controller_drop_in_at_horizon_40(cuda):
