@@ -158,6 +158,50 @@ class BatchedMPCController:
         return BatchSolution(self._u0[:B], self._X[:B], self._U[:B], self._status[:B], self._iters[:B],
                              self._active[:B])
 
+    def solve_one(self, x0, ref, u_prev=None):
+        """One QP with one packed host->device copy, one device->host copy and one sync (the
+        sequential closed loop of ``TrajectoryTracker.track``: the copies dominate a B=1 step).
+        ``x0`` (4,), ``ref`` (N+1, 4), ``u_prev`` (2,) host arrays.  Returns host numpy
+        ``(status, u0, X, U)``; X (4, N+1) and U (2, N) are fresh arrays."""
+        torch = self._torch
+        N = self.horizon
+        io = getattr(self, "_one", None)
+        if io is None:
+            nin = 4 + 4 * (N + 1) + 2
+            # outputs packed in one byte block: u0 | X | U (float64), status | iters (int32), active (u8)
+            offs = {"u0": 0, "X": 16, "U": 16 + 32 * (N + 1)}
+            offs["status"] = offs["U"] + 16 * N
+            offs["iters"] = offs["status"] + 4
+            offs["active"] = offs["iters"] + 16
+            nout = offs["active"] + 5 * N + 1
+            hin = torch.empty(nin, dtype=torch.float64, pin_memory=True)
+            hout = torch.empty(nout, dtype=torch.uint8, pin_memory=True)
+            io = self._one = dict(
+                hin=hin, hin_np=hin.numpy(), din=torch.empty(nin, dtype=torch.float64, device=self.device),
+                hout=hout, hout_np=hout.numpy(), dout=torch.empty(nout, dtype=torch.uint8, device=self.device),
+                offs=offs)
+        h = io["hin_np"]
+        h[0:4] = np.asarray(x0, dtype=np.float64).reshape(4)
+        h[4:4 + 4 * (N + 1)] = np.asarray(ref, dtype=np.float64).reshape(-1)[: 4 * (N + 1)]
+        h[4 + 4 * (N + 1):] = 0.0 if u_prev is None else np.asarray(u_prev, dtype=np.float64).reshape(2)
+        stream = torch.cuda.current_stream(self.device)
+        s = ctypes.c_void_p(stream.cuda_stream)
+        din, dout, o = io["din"], io["dout"], io["offs"]
+        din.copy_(io["hin"], non_blocking=True)
+        d = din.data_ptr()
+        _lib.check(self._L.mpcqp_build(self._ws, 1, d, d + 32, d + 32 * (N + 2), s), "mpcqp_build")
+        b = dout.data_ptr()
+        _lib.check(self._L.mpcqp_solve(self._ws, 1, b + o["u0"], b + o["X"], b + o["U"], b + o["status"],
+                                       b + o["iters"], b + o["active"], s), "mpcqp_solve")
+        io["hout"].copy_(dout, non_blocking=True)
+        stream.synchronize()
+        hb = io["hout_np"]
+        status = int(np.frombuffer(hb, np.int32, 1, o["status"])[0])
+        u0 = np.frombuffer(hb, np.float64, 2, o["u0"]).copy()
+        X = np.frombuffer(hb, np.float64, 4 * (N + 1), o["X"]).reshape(4, N + 1).copy()
+        U = np.frombuffer(hb, np.float64, 2 * N, o["U"]).reshape(2, N).copy()
+        return status, u0, X, U
+
     def close(self) -> None:
         if getattr(self, "_ws", None) is not None and self._ws.value:
             self._L.mpcqp_destroy(self._ws)
@@ -216,16 +260,13 @@ class MPCController:
         ref = ref[: N + 1]
         up = np.zeros((1, 2)) if u_prev is None else np.asarray(u_prev, dtype=float).reshape(1, 2)
         ctrl = _single_controller(self._params, **self._settings)
-        sol = ctrl.solve_batch(x0, ref[None], up)
-        status = int(sol.status.cpu()[0])
+        status, _, X, U = ctrl.solve_one(x0[0], ref, up[0])
         if status == _lib.NUMERICAL_ERROR:
             LOG.error("MPC solve failed with a numerical error")
             return None, None, None
         if status not in (_lib.SOLVED, _lib.SOLVED_INACCURATE):
             LOG.warning("MPC solve returned status %s", _lib.STATUS_NAMES.get(status, status))
             return None, None, None
-        U = sol.U[0].cpu().numpy().copy()
-        X = sol.X[0].cpu().numpy().copy()
         return U[:, 0].copy(), X, U
 
     @property
