@@ -38,6 +38,20 @@ __global__ __launch_bounds__(kWave) void k_build(mpcqp_params p, int B, const do
   if (b >= B) return;
   const int N = p.horizon;
   const double* rb = ref + (size_t)b * (N + 1) * 4;
+  const double x0l = lane < 4 ? x0[(size_t)b * 4 + lane] : 0.0;
+  const double upl = (lane >= 4 && lane < 6 && u_prev) ? u_prev[(size_t)b * 2 + lane - 4] : 0.0;
+  if (N + 1 > kWave) {  // long windows: chunks of 64 rows
+    build_qp_long(
+        p, lane,
+        [&](int k, double& rx, double& ry, double& ryaw, double& rv) {
+          rx = rb[4 * k + 0];
+          ry = rb[4 * k + 1];
+          ryaw = rb[4 * k + 2];
+          rv = rb[4 * k + 3];
+        },
+        x0l, upl, model + (size_t)b * model_stride(N));
+    return;
+  }
   double rx = 0.0, ry = 0.0, ryaw = 0.0, rv = 0.0;
   if (lane <= N) {
     rx = rb[4 * lane + 0];
@@ -45,8 +59,6 @@ __global__ __launch_bounds__(kWave) void k_build(mpcqp_params p, int B, const do
     ryaw = rb[4 * lane + 2];
     rv = rb[4 * lane + 3];
   }
-  const double x0l = lane < 4 ? x0[(size_t)b * 4 + lane] : 0.0;
-  const double upl = (lane >= 4 && lane < 6 && u_prev) ? u_prev[(size_t)b * 2 + lane - 4] : 0.0;
   build_qp(p, lane, rx, ry, ryaw, rv, x0l, upl, model + (size_t)b * model_stride(N));
 }
 

@@ -83,4 +83,68 @@ __device__ __forceinline__ void build_qp(const mpcqp_params& p, int lane, double
   if (lane < 6) mb[11 * N + 4 + lane] = lane < 4 ? x0l : upl;
 }
 
+// Windows longer than a wave (N + 1 > 64 rows, the long-horizon solve): build_lane + build_qp over
+// chunks of 64 rows (lane = row - base), the previous chunk's last raw yaw, unwrapped yaw, speed
+// and running unwrap sum carried in -- per row the same operations in the same order.
+// fetch(row, rx, ry, ryaw, rv) loads window row `row` <= N.  Every lane of the wave must call this.
+template <class Fetch>
+__device__ __forceinline__ void build_qp_long(const mpcqp_params& p, int lane, Fetch&& fetch, double x0l,
+                                              double upl, double* __restrict__ mb) {
+  const int N = p.horizon;
+  const double dt = p.dt, L = p.wheelbase_px;
+  const double sec2 = 1.0 / (1.0 * 1.0 + 1e-9);
+  double c_yaw = 0.0, c_uyaw = 0.0, c_rv = 0.0, cs = 0.0;  // carries from the previous chunk
+  for (int base = 0; base <= N; base += kWave) {
+    const int k = base + lane;
+    double rx = 0.0, ry = 0.0, ryaw = 0.0, rv = 0.0;
+    if (k <= N) fetch(k, rx, ry, ryaw, rv);
+    double prev = dpp<kWaveShr1>(ryaw);
+    if (lane == 0) prev = c_yaw;
+    double pc = 0.0;
+    if (k >= 1 && k <= N) {
+      const double dd = ryaw - prev;
+      double ddmod = np_mod(dd + kPi, kTwoPi) + (-kPi);
+      if (ddmod == -kPi && dd > 0.0) ddmod = kPi;
+      pc = ddmod - dd;
+      if (fabs(dd) < kPi) pc = 0.0;
+    }
+    // running sum in numpy's order; a chunk without a wrap leaves it unchanged (adding +0.0 to a
+    // sum that is never -0.0 keeps its bits)
+    double mine = cs;
+    if (wave_any(pc != 0.0))
+      for (int j = 0; j < kWave && base + j <= N; ++j) {
+        if (base + j >= 1) cs = cs + readlane(pc, j);
+        if (lane == j) mine = cs;
+      }
+    const double uyaw = k == 0 ? ryaw : ryaw + mine;
+    double psi = dpp<kWaveShr1>(uyaw), v = dpp<kWaveShr1>(rv);
+    if (lane == 0) {
+      psi = k == 0 ? uyaw : c_uyaw;
+      v = k == 0 ? rv : c_rv;
+    }
+    if (k <= N) {
+      mb[7 * N + 4 * k + 0] = rx;
+      mb[7 * N + 4 * k + 1] = ry;
+      mb[7 * N + 4 * k + 2] = uyaw;
+      mb[7 * N + 4 * k + 3] = rv;
+    }
+    if (k < N) {
+      double sn, c;
+      sincos(psi, &sn, &c);
+      const double al = -dt * v * sn, ga = dt * v * c;
+      mb[k] = al;
+      mb[N + k] = dt * c;
+      mb[2 * N + k] = ga;
+      mb[3 * N + k] = dt * sn;
+      mb[4 * N + k] = dt * (v / L) * sec2;
+      mb[5 * N + k] = -al * psi;
+      mb[6 * N + k] = -ga * psi;
+    }
+    c_yaw = readlane(ryaw, kWave - 1);
+    c_uyaw = readlane(uyaw, kWave - 1);
+    c_rv = readlane(rv, kWave - 1);
+  }
+  if (lane < 6) mb[11 * N + 4 + lane] = lane < 4 ? x0l : upl;
+}
+
 }  // namespace

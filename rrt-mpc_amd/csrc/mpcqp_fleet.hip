@@ -44,17 +44,23 @@ __global__ __launch_bounds__(kWave) void k_fleet_build(mpcqp_params p, mpcqp_fle
   if (!go) return;
   const int N = p.horizon;
   const int len = f.ref_len[b];
-  const int row = min(f.path_idx[b] + lane, len - 1);
-  double rx = 0.0, ry = 0.0, ryaw = 0.0, rv = 0.0;
-  if (lane <= N) {
-    const double* r = f.ref_global + ((size_t)b * f.ref_stride + row) * 4;
+  const int pidx = f.path_idx[b];
+  const double x0l = lane < 4 ? f.state[(size_t)b * 4 + lane] : 0.0;
+  const double upl = (lane >= 4 && lane < 6) ? f.u_prev[(size_t)b * 2 + lane - 4] : 0.0;
+  // window row k = ref[min(path_idx + k, len - 1)] (tail padding, control_stage.py:101-105)
+  auto fetch = [&](int k, double& rx, double& ry, double& ryaw, double& rv) {
+    const double* r = f.ref_global + ((size_t)b * f.ref_stride + min(pidx + k, len - 1)) * 4;
     rx = r[0];
     ry = r[1];
     ryaw = r[2];
     rv = relax ? r[3] * 0.6 : r[3];  // relaxed_reference[:, 3] *= 0.6 (control_stage.py:48-49)
+  };
+  if (N + 1 > kWave) {  // long windows: chunks of 64 rows
+    build_qp_long(p, lane, fetch, x0l, upl, model + (size_t)b * model_stride(N));
+    return;
   }
-  const double x0l = lane < 4 ? f.state[(size_t)b * 4 + lane] : 0.0;
-  const double upl = (lane >= 4 && lane < 6) ? f.u_prev[(size_t)b * 2 + lane - 4] : 0.0;
+  double rx = 0.0, ry = 0.0, ryaw = 0.0, rv = 0.0;
+  if (lane <= N) fetch(lane, rx, ry, ryaw, rv);
   build_qp(p, lane, rx, ry, ryaw, rv, x0l, upl, model + (size_t)b * model_stride(N));
 }
 

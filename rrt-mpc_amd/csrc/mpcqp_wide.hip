@@ -363,8 +363,37 @@ struct Wide {
     }
     __syncthreads();
   }
+  // The C code's sweep_inverse on K where it lives (n > 128: a column does not fit the
+  // register-resident sweep's 64 rows per thread): per pivot the column is copied, then every
+  // element updated exactly as the C code updates it, one barrier per pivot.
+  __device__ __forceinline__ bool sweep_mem() const {
+#pragma clang fp contract(off)
+    const int n = L.n;
+    double* col = A + L.oCol;
+    for (int k = 0; k < n; ++k) {
+      __syncthreads();
+      for (int i = tid; i < n; i += kT) col[i] = K(i, k);
+      __syncthreads();
+      const double d = col[k];
+      if (!(d > 0.0) || !isfinite(d)) return false;  // uniform
+      const double inv = 1.0 / d;
+      for_ij(n, tid, [&](int i, int j, int) {
+        if (i == k)
+          K(k, j) = j == k ? -inv : col[j] * inv;
+        else if (j == k)
+          K(i, k) = col[i] * inv;
+        else
+          K(i, j) = K(i, j) - (col[i] * inv) * col[j];
+      });
+    }
+    __syncthreads();
+    for_ij(n, tid, [&](int i, int j, int) { K(i, j) = -K(i, j); });  // A holds -A^{-1}
+    __syncthreads();
+    return true;
+  }
   __device__ __forceinline__ bool sweep() const {
     const int per = kT / L.n, chunk = (L.n + per - 1) / per;
+    if (chunk > 64) return sweep_mem();
     double *Kp = A + L.oK, *c0 = A + L.oCol, *c1 = A + L.oCol2;
     if (in_lds) {
       if (chunk <= 16) return sweep_regs<16, 3>(Kp, c0, c1, L.n, L.ks, tid);

@@ -10,7 +10,8 @@ and sums its line search in tree order.  Checks:
     statuses AND iteration counts identical bit for bit;
   * the fast mode against the same: statuses and active sets identical, U to 1e-8, ADMM
     iterations identical and all four counters on >= 95 % of QPs;
-  * the drop-in surface: MPCController(MPCConfig(horizon=40)) and a fleet at N = 40.
+  * the drop-in surface: MPCController(MPCConfig(horizon=40)) and a fleet at N = 40;
+  * horizons past a wave (N = 64..127): K1 in chunks of 64 rows, the sweep in memory past 2N = 128.
 """
 from __future__ import annotations
 
@@ -54,12 +55,12 @@ def _solve_with_model(params, x0, ref, u_prev, **settings):
     return out, model
 
 
-@pytest.mark.parametrize("N", [32, 40, 48, 63])
+@pytest.mark.parametrize("N", [32, 40, 48, 63, 64, 80, 127])
 def test_long_horizons_match_exact_oracle(cuda, N):
     import mpc_oracle as mo
     from mpcqp import scenarios
 
-    batch = scenarios.config3(24, horizon=N, seed=300 + N)
+    batch = scenarios.config3(24 if N < 64 else 8, horizon=N, seed=300 + N)
     params = _params(N)
     out, _ = _solve_with_model(params, batch.x0, batch.ref, batch.u_prev)
     assert (out["status"] == 1).all(), np.unique(out["status"], return_counts=True)
@@ -72,14 +73,15 @@ def test_long_horizons_match_exact_oracle(cuda, N):
 
 
 @pytest.mark.parametrize("N,settings", [(32, {}), (40, {}), (40, {"polish_near": 0.0}),
-                                        (48, {"polish_from": 0, "polish_near": 0.0}), (63, {})])
+                                        (48, {"polish_from": 0, "polish_near": 0.0}), (63, {}), (64, {}),
+                                        (90, {})])
 def test_long_horizons_bit_exact_with_c_restatement(cuda, N, settings):
     """Same model in -> same bits out: solutions, statuses, ADMM/polish/factorization/line-search
     counts all identical to oracle/mpcqp_cpu.c (100 % of QPs, not a majority)."""
     import cpu_solver
     from mpcqp import scenarios
 
-    batch = scenarios.config3(48, horizon=N, seed=700 + N)
+    batch = scenarios.config3(48 if N < 64 else 16, horizon=N, seed=700 + N)
     params = _params(N)
     out, model = _solve_with_model(params, batch.x0, batch.ref, batch.u_prev, reproducible=1, **settings)
     ref = cpu_solver.cpu_solve_models(params, model, **settings)
@@ -133,6 +135,28 @@ def test_reproducible_mode_bit_exact_with_c_restatement(cuda, N, config, setting
     assert np.array_equal(fast["active"], out["active"]) and _rel(fast["U"], out["U"]) <= REL_TOL
 
 
+@pytest.mark.parametrize("N", [63, 64, 100, 127])
+def test_long_window_k1_matches_restatement(cuda, N):
+    """K1 on windows longer than a wave (N + 1 > 64 rows: chunks of 64 with carries) against the
+    C restatement's build bit for bit, and numpy's unwrap, with 2 pi jumps inside and across chunks."""
+    import cpu_solver
+    from mpcqp import scenarios
+
+    batch = scenarios.config3(12, horizon=N, seed=40 + N)
+    ref = batch.ref.copy()
+    ref[::3, 30:, 2] += 2 * np.pi
+    ref[1::3, 64:, 2] -= 4 * np.pi
+    ref[2::3, 65:, 2] += 2 * np.pi
+    params = _params(N)
+    out, model = _solve_with_model(params, batch.x0, ref, batch.u_prev, reproducible=1)
+    cpu = cpu_solver.cpu_solve(params, batch.x0, ref, batch.u_prev, want_model=True)["model"]
+    # window rows (x, y, unwrapped yaw, v), x0 and u_prev bit for bit; the linearisation's
+    # coefficients to 1e-12 (device sincos vs the host libm)
+    assert np.array_equal(model[:, 7 * N: 11 * N + 10], cpu[:, 7 * N: 11 * N + 10])
+    assert np.array_equal(model[:, 7 * N + 2: 11 * N + 4: 4], np.unwrap(ref[:, :, 2], axis=1))
+    assert _rel(model[:, : 7 * N], cpu[:, : 7 * N]) <= 1e-12
+
+
 def test_long_horizon_newton_and_max_iter(cuda):
     """Method newton and an ADMM capped below convergence: statuses and counts as the C code."""
     import cpu_solver
@@ -172,15 +196,17 @@ def test_mpc_controller_drop_in_at_horizon_40(cuda):
     assert X.shape == (4, 41) and U.shape == (2, 40)
 
 
-def test_fleet_at_horizon_40(cuda):
-    """The device closed loop at N = 40 (k_fleet_build + the long-horizon solve) against the
-    oracle's restatement of control_stage.py:84-150 on the same plans."""
+@pytest.mark.parametrize("N", [40, 80])
+def test_fleet_at_long_horizons(cuda, N):
+    """The device closed loop at N = 40 and 80 (k_fleet_build -- in chunks of 64 window rows at
+    80 -- + the long-horizon solve) against the oracle's restatement of control_stage.py:84-150 on
+    the same plans."""
     import mpc_oracle as mo
     from mpcqp import scenarios
     from mpcqp.config import MPCConfig
     from mpcqp.pipeline.fleet import FleetTracker, initial_state
 
-    N, V, steps = 40, 4, 30
+    V, steps = 4, 30 if N <= 40 else 12
     paths, starts, goals = scenarios.fleet5(V, seed=21)
     mpc = MPCConfig(horizon=N, sim_steps=steps)
     ft = FleetTracker(mpc, map_resolution=0.8, max_vehicles=V, max_ref_len=200, device="cuda:0")
