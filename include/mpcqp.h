@@ -45,7 +45,7 @@ extern "C" {
 #define MPCQP_E_HIP (-4)         /* HIP runtime / launch error */
 #define MPCQP_E_STATE (-5)       /* mpcqp_solve before mpcqp_build of the same B */
 
-#define MPCQP_MAX_HORIZON 127    /* the long-horizon solve keeps 2N <= 256 variables on its 256 threads */
+#define MPCQP_MAX_HORIZON 1024   /* per-QP workspace 16 (2N)^2 bytes: 67 MB at N = 1024 */
 #define MPCQP_WIDE_MIN_HORIZON 32 /* N <= 31: one wave per QP (2N variables on the lanes, the KKT
                                      inverse in registers); N >= 32: one 256-thread workgroup per QP */
 

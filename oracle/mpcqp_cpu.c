@@ -37,7 +37,8 @@
 
 #include "../include/mpcqp.h"
 
-#define MAXN MPCQP_MAX_HORIZON
+/* static per-thread storage: the restatement stops at N = 127 (the GPU goes to MPCQP_MAX_HORIZON) */
+#define MAXN (MPCQP_MAX_HORIZON < 127 ? MPCQP_MAX_HORIZON : 127)
 #define MAXNV (2 * MAXN)
 #define MAXR (5 * MAXN)
 #define PI_D 3.141592653589793

@@ -392,8 +392,9 @@ struct Wide {
     return true;
   }
   __device__ __forceinline__ bool sweep() const {
-    const int per = kT / L.n, chunk = (L.n + per - 1) / per;
-    if (chunk > 64) return sweep_mem();
+    const int per = kT / L.n;  // threads per column (0 past 2N = 256)
+    if (per == 0 || (L.n + per - 1) / per > 64) return sweep_mem();
+    const int chunk = (L.n + per - 1) / per;
     double *Kp = A + L.oK, *c0 = A + L.oCol, *c1 = A + L.oCol2;
     if (in_lds) {
       if (chunk <= 16) return sweep_regs<16, 3>(Kp, c0, c1, L.n, L.ks, tid);

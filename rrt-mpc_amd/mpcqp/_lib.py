@@ -17,7 +17,7 @@ LIB_NAME = "libmpcqp.so"
 LIB_PATH = Path(os.environ.get("MPCQP_LIB", Path(__file__).resolve().parent / LIB_NAME))
 
 # constants mirrored from include/mpcqp.h
-MAX_HORIZON = 127
+MAX_HORIZON = 1024
 WIDE_MIN_HORIZON = 32  # MPCQP_WIDE_MIN_HORIZON: one 256-thread workgroup per QP from here on
 SOLVED = 1
 SOLVED_INACCURATE = 2

@@ -243,7 +243,7 @@ def test_empty_batch_and_errors(cuda):
     assert L.mpcqp_build(ctrl._ws, 5, x0.data_ptr(), ref.data_ptr(), None, None) == -3  # > max_batch
     assert L.mpcqp_solve(ctrl._ws, 3, None, None, None, st.data_ptr(), None, None, None) == -5  # B != built
     bad = _lib.to_c_params(params)
-    bad.horizon = 128  # past MPCQP_MAX_HORIZON
+    bad.horizon = 1025  # past MPCQP_MAX_HORIZON
     ws = ctypes.c_void_p()
     assert L.mpcqp_create(ctypes.byref(bad), 4, 0, ctypes.byref(ws)) == -2
     assert b"horizon" in L.mpcqp_last_error()

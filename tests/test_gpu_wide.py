@@ -157,6 +157,23 @@ def test_long_window_k1_matches_restatement(cuda, N):
     assert _rel(model[:, : 7 * N], cpu[:, : 7 * N]) <= 1e-12
 
 
+def test_horizon_past_the_thread_count(cuda):
+    """N = 200 (2N = 400 variables > 256 threads per QP: the in-memory sweep, chunked K1 and every
+    strided loop past one pass) against the exact oracle, through MPCController.solve."""
+    import mpc_oracle as mo
+    from mpcqp import scenarios
+    from mpcqp.control.mpc_controller import MPCController
+
+    N = 200
+    batch = scenarios.config3(2, horizon=N, seed=5)
+    params = _params(N)
+    for b in range(batch.size):
+        u0, X, U = MPCController(params).solve(batch.x0[b], batch.ref[b], u_prev=batch.u_prev[b])
+        ex = mo.solve_exact(params, batch.x0[b], batch.ref[b], batch.u_prev[b])
+        assert ex.converged and U is not None
+        assert max(_rel(U, ex.Umat), _rel(X, ex.X)) <= REL_TOL
+
+
 def test_long_horizon_newton_and_max_iter(cuda):
     """Method newton and an ADMM capped below convergence: statuses and counts as the C code."""
     import cpu_solver
