@@ -103,3 +103,27 @@ def test_batched_controller_reuses_device_inputs(cuda):
     assert (sol.status == 1).all().item()
     np.testing.assert_array_equal(sol.u0.cpu().numpy(), sol.U[:, :, 0].cpu().numpy())
     ctrl.close()
+
+
+def test_solve_one_equals_solve_batch(cuda):
+    """The B=1 drop-in's packed-transfer path (BatchedMPCController.solve_one, behind
+    MPCController.solve) returns exactly what solve_batch returns for the same QP, at a fused
+    (N = 20) and a long (N = 40) horizon, including the unsolvable case's status."""
+    from mpcqp import _lib, scenarios
+    from mpcqp.config import MPCConfig
+    from mpcqp.control.mpc_controller import BatchedMPCController
+
+    for N in (20, 40):
+        b = scenarios.config3(4, horizon=N, seed=11)
+        ref = b.ref.copy()
+        ref[3, 2:, 0] = np.nan  # status numerical_error
+        ctrl = BatchedMPCController(MPCConfig(horizon=N).to_parameters(0.8), 4, device="cuda:0")
+        sol = ctrl.solve_batch(b.x0, ref, b.u_prev)
+        st, U, X = sol.status.cpu().numpy(), sol.U.cpu().numpy(), sol.X.cpu().numpy()
+        for q in range(4):
+            status, u0, Xq, Uq = ctrl.solve_one(b.x0[q], ref[q], b.u_prev[q])
+            assert status == st[q]
+            if status == _lib.SOLVED:
+                assert np.array_equal(Uq, U[q]) and np.array_equal(Xq, X[q]) and np.array_equal(u0, U[q][:, 0])
+        assert st[3] == _lib.NUMERICAL_ERROR
+        ctrl.close()
