@@ -12,6 +12,7 @@ from __future__ import annotations
 
 import ctypes
 import logging
+import os
 from collections import OrderedDict
 from dataclasses import dataclass
 from typing import NamedTuple, Optional, Tuple
@@ -159,42 +160,38 @@ class BatchedMPCController:
                              self._active[:B])
 
     def solve_one(self, x0, ref, u_prev=None):
-        """One QP with one packed host->device copy, one device->host copy and one sync (the
-        sequential closed loop of ``TrajectoryTracker.track``: the copies dominate a B=1 step).
-        ``x0`` (4,), ``ref`` (N+1, 4), ``u_prev`` (2,) host arrays.  Returns host numpy
-        ``(status, u0, X, U)``; X (4, N+1) and U (2, N) are fresh arrays."""
+        """One QP for the sequential closed loop of ``TrajectoryTracker.track``, where the copies
+        dominate a B=1 step.  Inputs and outputs are packed into one block each of pinned,
+        device-mapped host memory that the kernels read and write in place: no copy commands,
+        one stream sync.  (``MPCQP_B1_STAGING=copy`` stages through device buffers instead: one
+        host->device and one device->host copy.)  ``x0`` (4,), ``ref`` (N+1, 4), ``u_prev`` (2,)
+        host arrays.  Returns host numpy ``(status, u0, X, U)``; X (4, N+1) and U (2, N) are fresh
+        arrays."""
         torch = self._torch
         N = self.horizon
         io = getattr(self, "_one", None)
         if io is None:
-            nin = 4 + 4 * (N + 1) + 2
-            # outputs packed in one byte block: u0 | X | U (float64), status | iters (int32), active (u8)
-            offs = {"u0": 0, "X": 16, "U": 16 + 32 * (N + 1)}
-            offs["status"] = offs["U"] + 16 * N
-            offs["iters"] = offs["status"] + 4
-            offs["active"] = offs["iters"] + 16
-            nout = offs["active"] + 5 * N + 1
-            hin = torch.empty(nin, dtype=torch.float64, pin_memory=True)
-            hout = torch.empty(nout, dtype=torch.uint8, pin_memory=True)
-            io = self._one = dict(
-                hin=hin, hin_np=hin.numpy(), din=torch.empty(nin, dtype=torch.float64, device=self.device),
-                hout=hout, hout_np=hout.numpy(), dout=torch.empty(nout, dtype=torch.uint8, device=self.device),
-                offs=offs)
+            io = self._one = self._one_buffers()
         h = io["hin_np"]
         h[0:4] = np.asarray(x0, dtype=np.float64).reshape(4)
         h[4:4 + 4 * (N + 1)] = np.asarray(ref, dtype=np.float64).reshape(-1)[: 4 * (N + 1)]
         h[4 + 4 * (N + 1):] = 0.0 if u_prev is None else np.asarray(u_prev, dtype=np.float64).reshape(2)
         stream = torch.cuda.current_stream(self.device)
         s = ctypes.c_void_p(stream.cuda_stream)
-        din, dout, o = io["din"], io["dout"], io["offs"]
-        din.copy_(io["hin"], non_blocking=True)
-        d = din.data_ptr()
+        o = io["offs"]
+        if io["mapped"]:
+            d, b = io["din_ptr"], io["dout_ptr"]
+        else:
+            io["din"].copy_(io["hin"], non_blocking=True)
+            d, b = io["din"].data_ptr(), io["dout"].data_ptr()
         _lib.check(self._L.mpcqp_build(self._ws, 1, d, d + 32, d + 32 * (N + 2), s), "mpcqp_build")
-        b = dout.data_ptr()
         _lib.check(self._L.mpcqp_solve(self._ws, 1, b + o["u0"], b + o["X"], b + o["U"], b + o["status"],
                                        b + o["iters"], b + o["active"], s), "mpcqp_solve")
-        io["hout"].copy_(dout, non_blocking=True)
-        stream.synchronize()
+        if io["mapped"]:
+            _lib.check(_lib.hip().hipStreamSynchronize(s), "hipStreamSynchronize")
+        else:
+            io["hout"].copy_(io["dout"], non_blocking=True)
+            stream.synchronize()
         hb = io["hout_np"]
         status = int(np.frombuffer(hb, np.int32, 1, o["status"])[0])
         u0 = np.frombuffer(hb, np.float64, 2, o["u0"]).copy()
@@ -202,7 +199,38 @@ class BatchedMPCController:
         U = np.frombuffer(hb, np.float64, 2 * N, o["U"]).reshape(2, N).copy()
         return status, u0, X, U
 
+    def _one_buffers(self) -> dict:
+        torch = self._torch
+        N = self.horizon
+        nin = 4 + 4 * (N + 1) + 2
+        # outputs packed in one byte block: u0 | X | U (float64), status | iters (int32), active (u8)
+        offs = {"u0": 0, "X": 16, "U": 16 + 32 * (N + 1)}
+        offs["status"] = offs["U"] + 16 * N
+        offs["iters"] = offs["status"] + 4
+        offs["active"] = offs["iters"] + 16
+        nout = offs["active"] + 5 * N + 1
+        if os.environ.get("MPCQP_B1_STAGING", "mapped") != "copy":
+            with torch.cuda.device(self.device):
+                hin = _lib.MappedHostBuffer(8 * nin)
+                hout = _lib.MappedHostBuffer(nout)
+            return dict(mapped=True, hin_buf=hin, hout_buf=hout, hin_np=hin.array(np.float64, nin),
+                        hout_np=hout.array(np.uint8, nout), din_ptr=hin.dev.value, dout_ptr=hout.dev.value,
+                        offs=offs)
+        hin = torch.empty(nin, dtype=torch.float64, pin_memory=True)
+        hout = torch.empty(nout, dtype=torch.uint8, pin_memory=True)
+        return dict(mapped=False, hin=hin, hin_np=hin.numpy(),
+                    din=torch.empty(nin, dtype=torch.float64, device=self.device),
+                    hout=hout, hout_np=hout.numpy(), dout=torch.empty(nout, dtype=torch.uint8, device=self.device),
+                    offs=offs)
+
     def close(self) -> None:
+        io = getattr(self, "_one", None)
+        if io is not None and io["mapped"]:
+            if self._ws is not None and self._ws.value:
+                self._torch.cuda.synchronize(self.device)  # nothing may still read or write the blocks
+            io["hin_buf"].free()
+            io["hout_buf"].free()
+            self._one = None
         if getattr(self, "_ws", None) is not None and self._ws.value:
             self._L.mpcqp_destroy(self._ws)
             self._ws = ctypes.c_void_p()
