@@ -105,10 +105,13 @@ def test_batched_controller_reuses_device_inputs(cuda):
     ctrl.close()
 
 
-def test_solve_one_equals_solve_batch(cuda):
-    """The B=1 drop-in's packed-transfer path (BatchedMPCController.solve_one, behind
-    MPCController.solve) returns exactly what solve_batch returns for the same QP, at a fused
-    (N = 20) and a long (N = 40) horizon, including the unsolvable case's status."""
+@pytest.mark.parametrize("staging", ["mapped", "copy"])
+def test_solve_one_equals_solve_batch(cuda, monkeypatch, staging):
+    """The B=1 drop-in (BatchedMPCController.solve_one, behind MPCController.solve) returns
+    exactly what solve_batch returns for the same QP, at a fused (N = 20) and a long (N = 40)
+    horizon, including the unsolvable case's status: kernels reading and writing mapped host
+    memory in place, and the staged variant (one copy each way)."""
+    monkeypatch.setenv("MPCQP_B1_STAGING", staging)
     from mpcqp import _lib, scenarios
     from mpcqp.config import MPCConfig
     from mpcqp.control.mpc_controller import BatchedMPCController
@@ -122,6 +125,7 @@ def test_solve_one_equals_solve_batch(cuda):
         st, U, X = sol.status.cpu().numpy(), sol.U.cpu().numpy(), sol.X.cpu().numpy()
         for q in range(4):
             status, u0, Xq, Uq = ctrl.solve_one(b.x0[q], ref[q], b.u_prev[q])
+            assert ctrl._one["mapped"] == (staging == "mapped")
             assert status == st[q]
             if status == _lib.SOLVED:
                 assert np.array_equal(Uq, U[q]) and np.array_equal(Xq, X[q]) and np.array_equal(u0, U[q][:, 0])
