@@ -287,8 +287,15 @@ class MPCController:
             raise ValueError(f"ref_traj must have shape (>= {N + 1}, 4), got {ref.shape}")
         ref = ref[: N + 1]
         up = np.zeros((1, 2)) if u_prev is None else np.asarray(u_prev, dtype=float).reshape(1, 2)
+        # A missing library or device fails loudly here (no CPU fallback exists) ...
         ctrl = _single_controller(self._params, **self._settings)
-        status, _, X, U = ctrl.solve_one(x0[0], ref, up[0])
+        try:
+            status, _, X, U = ctrl.solve_one(x0[0], ref, up[0])
+        except _lib.LibraryError:
+            # ... while a failed launch of the solve maps to (None, None, None), as the
+            # reference maps cp.SolverError (mpc_controller.py:133-135).
+            LOG.exception("GPU failed during MPC solve")
+            return None, None, None
         if status == _lib.NUMERICAL_ERROR:
             LOG.error("MPC solve failed with a numerical error")
             return None, None, None

@@ -22,11 +22,27 @@ from ..control.vehicle_model import f_discrete
 LOG = logging.getLogger(__name__)
 
 
+def _reference_tracking_result():
+    """The reference's own ``TrackingResult`` when this module runs inside the reference tree
+    (``src/pipeline/artifacts.py:33-38``), so ``PipelineResult`` holds the class it declares."""
+    try:  # pragma: no cover - only inside the reference tree
+        from src.pipeline.artifacts import TrackingResult as ref_cls  # type: ignore
+
+        return ref_cls
+    except Exception:
+        return None
+
+
 @dataclass
 class TrackingResult:
-    """``src/pipeline/artifacts.py:33-38``."""
+    """``src/pipeline/artifacts.py:33-38`` (returned outside the reference tree; inside it,
+    ``track`` returns the reference's own class)."""
 
     states: Sequence[np.ndarray] = field(default_factory=list)
+
+# MapConfig.map_resolution default (src/config.py:22): the px/m scale step() assumes before any
+# track() call has fixed the parameters.
+DEFAULT_MAP_RESOLUTION = 0.8
 
 
 def _viz_hooks():
@@ -61,6 +77,8 @@ class TrajectoryTracker:
     # reference constructs TrajectoryTracker(mpc, viz) and gets the library defaults.
     solver_settings: dict = field(default_factory=dict)
     relaxed_solver_settings: dict = field(default_factory=dict)
+    # parameters of the last track() call; step() without params solves with them
+    _params: Optional[MPCParameters] = field(default=None, init=False, repr=False, compare=False)
 
     def _solve_with_relaxation(
         self,
@@ -98,13 +116,21 @@ class TrajectoryTracker:
     ) -> Tuple[Optional[np.ndarray], Optional[np.ndarray], Optional[np.ndarray]]:
         """One closed-loop iteration (``control_stage.py:107-129``): solve, then the plant step.
 
+        ``step(state, ref_window, u_prev)`` is the contract of SURVEY.md §8b.  The parameters are,
+        in order: ``params`` when given; ``self.mpc.to_parameters(map_resolution)`` when a
+        resolution is given; those of the last ``track()`` call; else
+        ``self.mpc.to_parameters(0.8)`` (the reference's ``MapConfig.map_resolution`` default).
+
         Returns ``(next_state, u0, Xp)``, or ``(None, None, None)`` when the QP stays
         unsolved after relaxation (the caller aborts, as ``:108-110`` does).
         """
         if params is None:
-            if map_resolution is None:
-                raise ValueError("step() needs params or map_resolution")
-            params = self.mpc.to_parameters(map_resolution)
+            if map_resolution is not None:
+                params = self.mpc.to_parameters(map_resolution)
+            elif self._params is not None:
+                params = self._params
+            else:
+                params = self._params = self.mpc.to_parameters(DEFAULT_MAP_RESOLUTION)
         u0, Xp, _ = self._solve_with_relaxation(state, ref_window, u_prev, params)
         if u0 is None or Xp is None:
             return None, None, None
@@ -128,7 +154,7 @@ class TrajectoryTracker:
         if not plan.path:
             raise RuntimeError("Planner returned an empty path")
 
-        base_params = self.mpc.to_parameters(map_resolution)
+        base_params = self._params = self.mpc.to_parameters(map_resolution)
         horizon = base_params.horizon
         wheelbase_px = base_params.wheelbase_px
 
@@ -195,7 +221,7 @@ class TrajectoryTracker:
                 break
 
         LOG.info("MPC tracking finished after %d steps (goal_reached=%s)", len(states), goal_reached)
-        return TrackingResult(states=states)
+        return (_reference_tracking_result() or TrackingResult)(states=states)
 
 
 __all__ = ["TrajectoryTracker", "TrackingResult", "window_at"]

@@ -68,6 +68,25 @@ def test_step_is_one_loop_iteration(cuda, golden):
         assert Xp.shape == (4, 16)
 
 
+def test_three_argument_step_reproduces_reference_loop(cuda, golden):
+    """SURVEY §8b's contract ``step(state, ref_window, u_prev) -> (next_state, u0, X)``: no params
+    argument, so the tracker uses ``MPCConfig.to_parameters(0.8)`` (the reference's
+    ``MapConfig.map_resolution`` default) -- the resolution closed_loop.npz was generated at.
+    Every one of the 65 recorded N = 15 windows of the reference's own loop is replayed."""
+    from mpcqp.config import MPCConfig, VizConfig
+    from mpcqp.pipeline.control_stage import TrajectoryTracker
+
+    loop = golden("closed_loop.npz")
+    assert float(golden("default_plan.npz")["map_resolution"]) == 0.8
+    tracker = TrajectoryTracker(MPCConfig(horizon=15), VizConfig())
+    for k in range(len(loop["N15_x0"])):
+        nxt, u0, Xp = tracker.step(loop["N15_x0"][k], loop["N15_window"][k], loop["N15_u_prev"][k])
+        np.testing.assert_allclose(u0, loop["N15_u0"][k], rtol=0, atol=1e-8)
+        np.testing.assert_allclose(nxt, loop["N15_states"][k], rtol=0, atol=1e-8)
+        assert Xp.shape == (4, 16)
+        np.testing.assert_array_equal(Xp[:, 0], loop["N15_x0"][k])
+
+
 def test_unsolvable_input_takes_the_relaxation_path_and_aborts(cuda, caplog):
     """Non-finite data -> status numerical_error -> relaxation retry (control_stage.py:45-56)
     -> still None -> (None, None, None), as the reference's loop expects (:108-110)."""

@@ -273,3 +273,42 @@ def test_solver_kernel_resources():
         assert r["Occupancy"] >= (2 if N <= 28 else 1), (N, r)
         assert r["AGPRs"] == 0 or N >= 29, (N, r)
         assert r["ScratchSize"] == 0, (N, r)
+
+
+def test_three_argument_step_resolves_parameters(golden, monkeypatch):
+    """``TrajectoryTracker.step(state, ref_window, u_prev)`` on the host logic: the
+    B=1 device call swapped for the C restatement (no GPU here), every N = 15 window of the
+    reference's own loop replayed without a params argument (-> ``to_parameters(0.8)``); after a
+    ``track()`` at another resolution the tracker keeps that call's parameters."""
+    import mpcqp.control.mpc_controller as mc
+    from mpcqp.config import MPCConfig, VizConfig
+    from mpcqp.pipeline.control_stage import TrajectoryTracker
+
+    from _dropin_driver import _CpuSingle
+
+    seen = []
+
+    def single(params, method="admm", **settings):
+        seen.append(float(params.wheelbase_px))
+        return _CpuSingle(params, **settings)
+
+    monkeypatch.setattr(mc, "_single_controller", single)
+    loop = golden("closed_loop.npz")
+    tracker = TrajectoryTracker(MPCConfig(horizon=15), VizConfig())
+    for k in range(len(loop["N15_x0"])):
+        nxt, u0, Xp = tracker.step(loop["N15_x0"][k], loop["N15_window"][k], loop["N15_u_prev"][k])
+        np.testing.assert_allclose(u0, loop["N15_u0"][k], rtol=0, atol=1e-8)
+        np.testing.assert_allclose(nxt, loop["N15_states"][k], rtol=0, atol=1e-8)
+        assert Xp.shape == (4, 16)
+    assert set(seen) == {2.8 / 0.8}
+    tracker.step(loop["N15_x0"][0], loop["N15_window"][0], loop["N15_u_prev"][0], map_resolution=0.2)
+    assert seen[-1] == 2.8 / 0.2
+    plan = golden("default_plan.npz")
+    from types import SimpleNamespace
+
+    planning = SimpleNamespace(plan=SimpleNamespace(success=True, path=[tuple(map(float, p)) for p in plan["path"]]))
+    maps = SimpleNamespace(start=tuple(plan["start"]), goal=tuple(plan["goal"]))
+    tracker.mpc = MPCConfig(horizon=15, sim_steps=1)
+    tracker.track(planning, maps, map_resolution=0.4, visualize=False)
+    tracker.step(loop["N15_x0"][0], loop["N15_window"][0], loop["N15_u_prev"][0])
+    assert seen[-1] == seen[-2] == 2.8 / 0.4
