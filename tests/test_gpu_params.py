@@ -15,10 +15,9 @@ and device fleet both return the oracle's optimum of the relaxed problem on the 
 """
 from __future__ import annotations
 
-from dataclasses import replace
-
 import numpy as np
 import pytest
+from param_variants import VARIANTS
 
 pytestmark = pytest.mark.gpu
 
@@ -33,42 +32,9 @@ def _base(N, res=0.8):
 
 
 def _variant(name, N):
-    from mpcqp.pipeline.fleet import relaxed_parameters
+    from param_variants import resolution, variant
 
-    p = _base(N, 0.2 if name == "wheelbase_14px" else 0.8)
-    if name == "q_nondiag":
-        q = np.array(p.q, float)
-        q[0, 1] = q[1, 0] = 1.5
-        q[2, 3] = q[3, 2] = 0.1
-        q[0, 2] = q[2, 0] = 0.3
-        qn = np.array(p.q_terminal, float)
-        qn[0, 1] = qn[1, 0] = 3.0
-        qn[1, 3] = qn[3, 1] = 0.15
-        assert np.linalg.eigvalsh(q).min() > 0 and np.linalg.eigvalsh(qn).min() > 0
-        return replace(p, q=q, q_terminal=qn)
-    if name == "r_offdiag":
-        r = np.array([[0.03, 0.02], [0.02, 0.25]])
-        return replace(p, r=r)
-    if name == "dt_0.05":
-        return replace(p, dt=0.05)
-    if name == "dt_0.2":
-        return replace(p, dt=0.2)
-    if name == "wheelbase_14px":
-        return p
-    if name == "tight_bounds":
-        return replace(p, u_bounds=((-5.0, 4.0), (-0.3, 0.25)), v_bounds=(2.0, 18.0),
-                       du_bounds=((-3.0, 2.5), (-0.05, 0.04)))
-    if name == "slack_x10":
-        return replace(p, slack_velocity=1e4, slack_input=5e3, slack_rate=5e3)
-    if name == "slack_div10":
-        return replace(p, slack_velocity=1e2, slack_input=50.0, slack_rate=50.0)
-    if name == "relaxed_du":
-        return relaxed_parameters(p)
-    raise KeyError(name)
-
-
-VARIANTS = ["q_nondiag", "r_offdiag", "dt_0.05", "dt_0.2", "wheelbase_14px", "tight_bounds", "slack_x10",
-            "slack_div10", "relaxed_du"]
+    return variant(_base(N, resolution(name)), name)
 
 
 def _solve(params, x0, ref, u_prev, **settings):
