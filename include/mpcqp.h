@@ -128,7 +128,9 @@ int mpcqp_num_rows(int horizon);
 int mpcqp_create(const mpcqp_params* p, int max_batch, int device, mpcqp_ws** ws);
 
 /* Replace the parameter block (same horizon), e.g. for the relaxation retry of
- * control_stage.py:45-55.  Stream-ordered with respect to later launches. */
+ * control_stage.py:45-55.  Stream-ordered with respect to later launches.  Invalidates the last
+ * mpcqp_build: the next mpcqp_solve returns MPCQP_E_STATE until mpcqp_build runs again, so a
+ * build is always solved with the parameters it was made with. */
 int mpcqp_set_params(mpcqp_ws* ws, const mpcqp_params* p);
 
 void mpcqp_destroy(mpcqp_ws* ws);

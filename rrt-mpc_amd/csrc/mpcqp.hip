@@ -182,6 +182,11 @@ int mpcqp_set_params(mpcqp_ws* ws, const mpcqp_params* p) {
   if (p->horizon != ws->p.horizon) return fail(MPCQP_E_HORIZON, "set_params cannot change the horizon");
   if (p->reproducible != ws->p.reproducible) return fail(MPCQP_E_ARG, "set_params cannot change reproducible");
   ws->p = *p;
+  // A build belongs to the parameter block it was made with (the fused solve derives its LTV model
+  // from the params in effect at solve time, the K1 kernel from those at build time): new params
+  // invalidate it, and the next mpcqp_solve needs a new mpcqp_build.
+  ws->built_B = -1;
+  ws->in_x0 = ws->in_ref = ws->in_up = nullptr;
   return MPCQP_OK;
 }
 

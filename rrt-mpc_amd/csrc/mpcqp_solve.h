@@ -8,22 +8,6 @@ using mpcqp::Launch;
 // The model block stays in LDS for the outputs (finish_qp) while Pbar is live, where that costs no
 // occupancy (8 workgroups of Pbar + model fit a CU's 160 KB of LDS: N <= 23); past that, the model shares
 // the setup's union with Pbar and the outputs re-derive it (K1 fused) or re-read it (workspace).
-#ifndef MPCQP_MODEL_KEEP  // development switch (A/B builds): 0 never keeps the model in LDS
-#define MPCQP_MODEL_KEEP 1
-#endif
-// Development switches (A/B builds).  MPCQP_BCAST_LDS 1 stages the dense products' broadcasts
-// through LDS (no VALU work) instead of permlane swaps: measured slower (B=4096 +3 %, B=512 +9 %:
-// the LDS round trip is on every product's critical path).  MPCQP_PIVOT_SGPR 1 reads the sweep's
-// pivot by readlane (off the broadcast's critical path) instead of from the broadcast copy.
-#ifndef MPCQP_BCAST_LDS
-#define MPCQP_BCAST_LDS 0
-#endif
-#ifndef MPCQP_PIVOT_SGPR
-#define MPCQP_PIVOT_SGPR 1
-#endif
-#ifndef MPCQP_BCAST_LDS_SWEEP  // ... for the sweep's pivot columns
-#define MPCQP_BCAST_LDS_SWEEP MPCQP_BCAST_LDS
-#endif
 template <int N>
 struct SolveSmem {
   static constexpr int n = 2 * N;
@@ -36,7 +20,7 @@ struct SolveSmem {
 
 template <int N>
 constexpr bool kModelKept =
-    MPCQP_MODEL_KEEP && 8 * (int)sizeof(SolveSmem<N>) + 8 * 8 * kWave + 64 * model_stride(N) <= 163840;
+    8 * (int)sizeof(SolveSmem<N>) + 64 * model_stride(N) <= 163840;
 
 template <int N>
 struct SetupSmem {
@@ -54,7 +38,6 @@ struct SolveLds {
     SetupSmem<N> setup;
     SolveSmem<N> solve;  // setup_qp writes Pbar when its own LDS data is dead
   };
-  double bc[kWave];  // broadcast staging of the dense row-per-lane products (Ctx::vbcast)
   double model[kModelKept<N> ? model_stride(N) : 1];  // the model block, live to the end (kModelKept)
   __device__ double* model_ptr() { return kModelKept<N> ? model : setup.model; }
 };
@@ -81,7 +64,6 @@ struct Ctx {
   double cscale;
   static constexpr int kPS = SolveSmem<N>::kPS;  // Pbar row stride
   double* __restrict__ P;  // Pbar (LDS, row-major n x n, row stride kPS)
-  double* __restrict__ bc;  // LDS broadcast staging (kWave doubles)
   const double* __restrict__ band;  // SolveSmem::band
   static constexpr int kNW = (n + 15) / 16;  // 16-lane rows holding the n variables
   // KKT inverse, row `lane`: A^{-1}[lane][j] = -r[j] (symmetric sweep operator)
@@ -91,9 +73,8 @@ struct Ctx {
 
   // Bind the context to this lane and the solve LDS (Pbar); the problem data fields are
   // filled by setup_qp.
-  __device__ __forceinline__ void init(int ln, double dt_, SolveSmem<N>& s, double* bcast_buf) {
+  __device__ __forceinline__ void init(int ln, double dt_, SolveSmem<N>& s) {
     lane = ln;
-    bc = bcast_buf;
     band = &s.band[0][0];
     n_full = 0;
     n_r1 = 0;
@@ -116,35 +97,11 @@ struct Ctx {
   }
 
   // Every lane's view of v (one element per lane): w[c] lane l = v[16 c + (l & 15)], read by the
-  // fmac_bc products through DPP row_newbcast.  Default: bcast() (permlane16/32 swaps + copies,
-  // ~12 VALU instructions, ~110 cycles).  LDS staging (one ds_write + kNW ds_reads, no VALU work;
-  // one wave per workgroup executes its LDS operations in order, so only compiler ordering points
-  // are needed) measured slower: its round trip is on every product's critical path.
-  template <bool LDS = MPCQP_BCAST_LDS>
-  __device__ __forceinline__ void vbcast(double v, double w[4]) const {
-    if constexpr (LDS) {
-    lds_sync();
-    bc[lane] = v;
-    lds_sync();
-    const double* b = bc + (lane & 15);
-    Unroll<0, kNW>::run([&](auto cc) {
-      constexpr int c = decltype(cc)::value;
-      w[c] = b[16 * c];
-    });
-    } else {
-      bcast<kNW>(v, w);
-    }
-  }
-  // element j of the vector last staged by vbcast<LDS>, in every lane
-  template <int J, bool LDS = MPCQP_BCAST_LDS>
-  __device__ __forceinline__ double staged(const double w[4]) const {
-    if constexpr (LDS) {
-      (void)w;
-      return bc[J];
-    } else {
-      return dpp<0x150 + (J % 16)>(w[J / 16]);
-    }
-  }
+  // fmac_bc products through DPP row_newbcast: bcast() (permlane16/32 swaps + copies, ~12 VALU
+  // instructions, ~110 cycles).  Staging through LDS instead (one ds_write + kNW ds_reads, no VALU
+  // work) measured slower (+3 % at B = 4096, +9 % at B = 512): its round trip is on every product's
+  // critical path.
+  __device__ __forceinline__ void vbcast(double v, double w[4]) const { bcast<kNW>(v, w); }
 
   // z = Cbar x: shifts only (no scans)
   __device__ __forceinline__ void Cmul(double x, double z[3]) const {
@@ -287,14 +244,9 @@ struct Ctx {
       // the pivot A[k][k] (lane k's r[k]): by readlane, so 1/d is computed while the column's
       // broadcast is in flight; then a vector reciprocal (v_rcp_f64 + two Newton steps, within an
       // ulp of 1/d): no IEEE division sequence on the step's critical path
-#if MPCQP_PIVOT_SGPR
       const double d = readlane(r[k], k);
-#endif
       double w[4];
-      vbcast<MPCQP_BCAST_LDS_SWEEP>(r[k], w);
-#if !MPCQP_PIVOT_SGPR
-      const double d = staged<k, MPCQP_BCAST_LDS_SWEEP>(w);
-#endif
+      vbcast(r[k], w);
       ok = ok && (d > 0.0) && isfinite(d);
       double inv = __builtin_amdgcn_rcp(d);
       inv = fma(inv, fma(-d, inv, 1.0), inv);
@@ -702,7 +654,7 @@ __device__ __forceinline__ bool setup_qp(const mpcqp_params& p, int b, const dou
   }
   // non-finite data (NaN/inf in x0, ref or u_prev) -> status MPCQP_NUMERICAL_ERROR
   const bool bad_input = wave_any(!finite);
-  C.init(lane, dt, lds.solve, lds.bc);
+  C.init(lane, dt, lds.solve);
   C.qv = qv;
   C.D = D;
   C.cscale = cscale;
@@ -773,10 +725,7 @@ __device__ __forceinline__ int polish_qp(Ctx<N>& C, double& x, const double zg[3
   double Px = C.Pmul(x);  // P x, carried along the passes
 #pragma unroll
   for (int r = 0; r < 3; ++r) cd[r] = zg[r] > C.hi[r] ? 2 : (zg[r] < C.lo[r] ? 1 : 0);
-#ifndef MPCQP_RANK1_DIV  // development switch: more than n / MPCQP_RANK1_DIV changed rows -> refactor
-#define MPCQP_RANK1_DIV 2
-#endif
-  constexpr int kMaxRank1 = n / MPCQP_RANK1_DIV;  // more changed rows than this: refactor (form + sweep)
+  constexpr int kMaxRank1 = n / 2;  // more changed rows than this: refactor (form + sweep)
   double rwf[3] = {0.0, 0.0, 0.0};  // soft-row weights of the current factorization
   bool have_fact = false;
   for (int pass = 0; pass < max_it; ++pass) {
@@ -1274,11 +1223,8 @@ __device__ __forceinline__ void finish_qp(const mpcqp_params& p, int b, const do
 // From N = 29 on the KKT inverse (2N doubles per lane) leaves 2 waves per SIMD no registers for
 // the rest of the working set, and Pbar (32 N^2 bytes of LDS) already limits a CU to 5
 // workgroups: the kernel takes the register file of 1 wave per SIMD instead of spilling.
-#ifndef MPCQP_ONE_WAVE_FROM
-#define MPCQP_ONE_WAVE_FROM 29
-#endif
 template <int N>
-constexpr int kSolveWavesPerEU = N >= MPCQP_ONE_WAVE_FROM ? 1 : 2;
+constexpr int kSolveWavesPerEU = N >= 29 ? 1 : 2;
 
 template <int N>
 __global__ __launch_bounds__(kWave, kSolveWavesPerEU<N>) void k_solve(mpcqp_params p, int B, const uint8_t* __restrict__ mask,

@@ -47,6 +47,8 @@ class SwarmResult:
     replan_steps: Optional[np.ndarray] = None  # (V, max_replans): steps[v] at replan r, -steps-1 failed, 0 unused
     last_replan_start: Optional[np.ndarray] = None  # (V, 2): where the last replan started
     last_replan_path: List[Optional[np.ndarray]] = field(default_factory=list)  # its final path (None: failed/none)
+    # the last replan failed because its smoothed path exceeded path_cap (not an RRT* failure)
+    replan_over_capacity: Optional[np.ndarray] = None
     inputs: List[np.ndarray] = field(default_factory=list)  # per vehicle: applied u0 per step
     timings: Dict[str, float] = field(default_factory=dict)
 
@@ -54,7 +56,11 @@ class SwarmResult:
 class Swarm:
     def __init__(self, occupancy: np.ndarray, mpc, planner: PlannerParameters, *, map_resolution: float,
                  max_vehicles: int, max_ref_len: int = 512, device=None, replan_distance: float = 15.0,
-                 max_replans: int = 2, path_cap: int = 2048, use_graph: bool = True) -> None:
+                 max_replans: int = 2, path_cap: int = 6144, use_graph: bool = True) -> None:
+        # path_cap: smoothed points a replan may produce.  The default is the most that the device
+        # reference builder stages (kRefCap, csrc/mpcqp_swarm.hip), so a replanned path is never cut
+        # shorter than a reference could be built from; capacity failures are reported apart from
+        # RRT* failures (SwarmResult.replan_over_capacity).
         self.occupancy = np.ascontiguousarray(occupancy, dtype=np.uint8)
         self.mpc = mpc
         self.planner = BatchedRRTStarPlanner(self.occupancy, planner, device=device)
@@ -168,14 +174,17 @@ class Swarm:
         sl = sb["smooth_len"][:V].cpu().numpy()
         smooth = sb["smooth"][:V].cpu().numpy()
         last_paths = []
+        over_cap = np.zeros(V, dtype=bool)
         for v in range(V):
+            over_cap[v] = bool(replans[v] and rsteps[v, replans[v] - 1] < 0 and sl[v] == -1)
             if replans[v] and rsteps[v, replans[v] - 1] >= 0 and sl[v] >= 1:
                 last_paths.append(smooth[v, : sl[v]].copy())
             else:
                 last_paths.append(None)
         return SwarmResult(states=r.states, phase=r.phase, steps=r.steps, replans=replans, planned=planned,
                            paths=found, replan_steps=rsteps, last_replan_start=sg[:, :2].copy(),
-                           last_replan_path=last_paths, inputs=r.inputs, timings=t)
+                           last_replan_path=last_paths, inputs=r.inputs, timings=t,
+                           replan_over_capacity=over_cap)
 
 
 # ------------------------------------------------------------------ multi-GPU: vehicles sharded over ranks
@@ -192,7 +201,8 @@ def shard_vehicles(V: int, world: int, rank: int) -> Tuple[int, int]:
     return lo, lo + base + (1 if rank < extra else 0)
 
 
-_PER_VEHICLE_ARRAYS = ("phase", "steps", "replans", "planned", "replan_steps", "last_replan_start")
+_PER_VEHICLE_ARRAYS = ("phase", "steps", "replans", "planned", "replan_steps", "last_replan_start",
+                       "replan_over_capacity")
 _PER_VEHICLE_LISTS = ("states", "paths", "last_replan_path", "inputs")
 
 

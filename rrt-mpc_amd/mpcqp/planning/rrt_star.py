@@ -337,6 +337,12 @@ class BatchedRRTStarPlanner:
             n = int(plen[v])
             if n == 0:
                 out.append(None)
+            elif smooth and n >= 2 and sl[v] == -1:
+                # the device smoothing's capacity (deduplicated points in LDS) is exceeded: the
+                # reference would smooth this path (rrt_star.py:264-273), so do not hand back the
+                # pruned one in its place
+                raise RuntimeError(f"problem {v}: pruned path of {n} points exceeds the device "
+                                   "Catmull-Rom capacity (mpcqp_catmull_rom returned -1)")
             elif smooth and n >= 2 and sl[v] >= 2:
                 out.append([tuple(map(float, q)) for q in sm[v, : sl[v]]])
             else:

@@ -247,6 +247,13 @@ def test_empty_batch_and_errors(cuda):
     ws = ctypes.c_void_p()
     assert L.mpcqp_create(ctypes.byref(bad), 4, 0, ctypes.byref(ws)) == -2
     assert b"horizon" in L.mpcqp_last_error()
+    # new parameters invalidate the last build: solving it would mix two parameter blocks
+    assert L.mpcqp_build(ctrl._ws, 2, x0.data_ptr(), ref.data_ptr(), None, None) == 0
+    assert L.mpcqp_set_params(ctrl._ws, ctypes.byref(_lib.to_c_params(params))) == 0
+    assert L.mpcqp_solve(ctrl._ws, 2, None, None, None, st.data_ptr(), None, None, None) == -5
+    assert L.mpcqp_build(ctrl._ws, 2, x0.data_ptr(), ref.data_ptr(), None, None) == 0
+    assert L.mpcqp_solve(ctrl._ws, 2, None, None, None, st.data_ptr(), None, None, None) == 0
+    torch.cuda.synchronize()
     ctrl.close()
 
 
