@@ -3,9 +3,13 @@ plans, device references, the fleet closed loop and the PER-STEP device replan t
 replanning itself on the device, end to end on the default inflated grid.
 
 Between replans every vehicle follows the reference's single-vehicle loop: a vehicle that was
-never replanned reproduces TrajectoryTracker.track on its own plan (1e-7 px); a replanned vehicle
-reproduces it up to the replan step, its new plan is RRTStarPlanner's from where it stood with its
-replan seed, and after the replan it reproduces the reference loop body on the new reference."""
+never replanned reproduces the oracle's restatement of TrajectoryTracker.track on its own plan
+(1e-7 px); a replanned vehicle reproduces it up to the replan step, its new plan is the reference
+planner's from where it stood with its replan seed, and after the replan it reproduces the
+reference loop body on the new reference.  The checkers run on the host only: the loop is
+mpc_oracle.track_loop / track_from with the C restatement's solves, the plans are
+oracle/rrt_oracle.grow_tree on the seed's own sample stream with oracle extraction and pruning --
+nothing in them touches the GPU."""
 from __future__ import annotations
 
 from types import SimpleNamespace
@@ -44,52 +48,78 @@ def _swarm(occ, V, sim_steps, **kw):
                  map_resolution=0.8, max_vehicles=V, device="cuda:0", **kw)
 
 
-def _host_track(path, start, goal, steps):
-    """TrajectoryTracker.track (control_stage.py:58-157) on one plan, B=1 GPU solves."""
-    from mpcqp.config import MPCConfig, VizConfig
-    from mpcqp.pipeline.control_stage import TrajectoryTracker
+def _c_solve(params, state, window, u_prev):
+    """One QP by the C restatement (oracle/mpcqp_cpu.c): no GPU in the checker."""
+    import cpu_solver
 
-    tr = TrajectoryTracker(MPCConfig(horizon=N_HORIZON, sim_steps=steps), VizConfig())
-    res = tr.track(SimpleNamespace(plan=SimpleNamespace(success=True, path=path)),
-                   SimpleNamespace(start=tuple(start), goal=tuple(goal)), map_resolution=0.8, visualize=False)
-    return np.asarray(res.states)
+    out = cpu_solver.cpu_solve(params, np.asarray(state, float)[None], np.asarray(window, float)[None],
+                               np.asarray(u_prev, float)[None], nthreads=1)
+    if out["status"][0] not in (1, 2):
+        return None, None, None
+    return out["u0"][0].copy(), out["X"][0].copy(), out["U"][0].copy()
+
+
+def _oracle_params():
+    import mpc_oracle as mo
+
+    return mo.default_params(N_HORIZON, 0.8)
+
+
+def _host_track(path, start, goal, steps):
+    """The reference's track loop (control_stage.py:79-150) restated by the oracle
+    (mpc_oracle.track_loop), every QP solved by the C restatement on the host."""
+    import mpc_oracle as mo
+    from mpcqp.control.ref_builder import build_reference
+
+    ref = build_reference(path, 15.0, N_HORIZON, 0.1)
+    yaw0 = float(np.arctan2(path[1][1] - path[0][1], path[1][0] - path[0][0])) if len(path) > 1 else 0.0
+    return np.asarray(mo.track_loop(_oracle_params(), ref, start, yaw0, goal, steps, solve_fn=_c_solve))
 
 
 def _host_continue(state, u_prev, path, goal, steps):
     """The loop body of control_stage.py:100-150 from a given state / u_prev on a new plan (the
-    swarm's replan: pose, speed and u_prev carry over, path_idx restarts at 0)."""
-    from mpcqp.config import MPCConfig, VizConfig
+    swarm's replan: pose, speed and u_prev carry over, path_idx restarts at 0) -- mpc_oracle.track_from
+    with the C restatement's solves."""
+    import mpc_oracle as mo
     from mpcqp.control.ref_builder import build_reference
-    from mpcqp.pipeline.control_stage import TrajectoryTracker, window_at
 
-    mpc = MPCConfig(horizon=N_HORIZON, sim_steps=steps)
-    tr = TrajectoryTracker(mpc, VizConfig())
-    params = mpc.to_parameters(0.8)
-    ref = build_reference(path, mpc.v_px_s, N_HORIZON, mpc.dt)
-    out, path_idx = [], 0
-    for _ in range(steps):
-        nxt, u0, _ = tr.step(state, window_at(ref, path_idx, N_HORIZON), u_prev, params)
-        if nxt is None:
-            break
-        state, u_prev = nxt, u0
-        out.append(state.copy())
-        if path_idx < len(ref) - 2:
-            dx, dy = state[0] - ref[path_idx][0], state[1] - ref[path_idx][1]
-            if dx * dx + dy * dy > 25.0:
-                path_idx += 1
-        if np.hypot(state[0] - goal[0], state[1] - goal[1]) < 8.0:
-            break
-    return np.asarray(out)
+    ref = build_reference(path, 15.0, N_HORIZON, 0.1)
+    return np.asarray(mo.track_from(_oracle_params(), ref, state, u_prev, goal, steps, solve_fn=_c_solve))
+
+
+def _oracle_plan(occ, start, goal, seed):
+    """RRTStarPlanner.plan (rrt_star.py:201-283) on the host: oracle/rrt_oracle.grow_tree fed the
+    seed's own sample stream (draw_samples), oracle extraction and shortcut pruning, then the
+    Catmull-Rom smoothing of the host restatement (pinned by branches.npz)."""
+    import rrt_oracle as ro
+    from mpcqp.common.geometry import catmull_rom_spline
+    from mpcqp.planning.rrt_star import draw_samples
+
+    prm = _planner_params(seed)
+    smp = draw_samples(int(seed), goal, occ.shape, prm.goal_sample_rate, prm.max_iterations)
+    nodes, _, gi = ro.grow_tree(occ, start, goal, smp, step=prm.step, goal_radius=prm.goal_radius,
+                                rewire_radius=prm.rewire_radius, collision_step=prm.collision_step)
+    if gi < 0:
+        return None
+    path = ro.extract_path(nodes, gi)
+    if prm.prune_path and len(path) >= 2:
+        pruned = ro.shortcut_prune(occ, path, prm.collision_step)
+        if len(pruned) >= 2:
+            path = pruned
+    if len(path) >= 2 and prm.spline_samples > 1:
+        spline = catmull_rom_spline(path, samples_per_segment=prm.spline_samples, alpha=prm.spline_alpha,
+                                    dedupe_tol=prm.dedupe_tolerance)
+        if len(spline) >= 2:
+            path = [tuple(map(float, q)) for q in spline]
+    return path
 
 
 def _check_plan(occ, start, goal, seed, path, tol=1e-4):
-    """The device plan against the reference planner's (RRTStarPlanner, host smoothing): same
+    """The device plan against the host restatement of the reference planner (_oracle_plan): same
     number of points, coordinates within the ~1e-5 px the duplicated end knots amplify an ulp to."""
-    from mpcqp.planning.rrt_star import RRTStarPlanner
-
-    plan = RRTStarPlanner(occ, _planner_params(seed)).plan(tuple(start), tuple(goal))
-    assert plan.success
-    ref = np.asarray(plan.path)
+    plan = _oracle_plan(occ, start, goal, seed)
+    assert plan is not None
+    ref = np.asarray(plan)
     got = np.asarray(path)
     assert ref.shape == got.shape, (ref.shape, got.shape)
     np.testing.assert_allclose(got, ref, rtol=0, atol=tol)
@@ -150,10 +180,11 @@ def test_swarm_vehicles_follow_the_reference_loop(cuda, golden):
 
 def test_per_step_replan_100_vehicles(cuda, golden):
     """BASELINE config 5 at its size: 100 vehicles on the default inflated grid, the trigger
-    evaluated on the device after EVERY step.  Every never-replanned vehicle equals
-    TrajectoryTracker.track on its own plan; every replanned vehicle equals it up to its replan
-    step, its new plan is the reference planner's from where it stood with its replan seed, and
-    from there it follows the reference loop body on the new reference."""
+    evaluated on the device after EVERY step.  Every initial plan is the reference planner's; every
+    never-replanned vehicle equals the reference loop (oracle restatement, C solves) on its own
+    plan; every replanned vehicle equals it up to its replan step, its new plan is the reference
+    planner's from where it stood with its replan seed, and from there it follows the reference
+    loop body on the new reference."""
     from mpcqp import _lib
     from mpcqp.pipeline.swarm import replan_seed
 
@@ -171,7 +202,9 @@ def test_per_step_replan_100_vehicles(cuda, golden):
         host = _host_track(res.paths[v], starts[v], goals[v], steps)
         assert res.steps[v] == len(host), v
         np.testing.assert_allclose(res.states[v], host, rtol=0, atol=1e-7)
-    for v in ok_replans[:12]:
+    for v in np.flatnonzero(res.planned):  # every initial plan: the reference planner's, seed v
+        _check_plan(occ, starts[v], goals[v], v, res.paths[v])
+    for v in ok_replans:
         s = int(res.replan_steps[v, 0])  # steps taken when the replan committed
         host = _host_track(res.paths[v], starts[v], goals[v], s)
         np.testing.assert_allclose(res.states[v][:s], host[:s], rtol=0, atol=1e-7)
