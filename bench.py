@@ -233,7 +233,7 @@ def host_threads() -> Tuple[int, int]:
     return threads, visible
 
 
-def spot_check(params, x0, ref, u_prev, U, active, status, idx) -> dict:
+def spot_check(params, x0, ref, u_prev, U, active, status, idx, iters=None) -> dict:
     """Checker: the GPU solutions of QPs `idx` against the C restatement, whose polish ends at the
     exact optimum of the QP (strictly convex: the same optimum OSQP+polish returns in the
     reference).  Parity against OSQP itself is unpinned here (OSQP is not installed)."""
@@ -246,7 +246,7 @@ def spot_check(params, x0, ref, u_prev, U, active, status, idx) -> dict:
     Uc = out["U"].reshape(len(idx), -1)
     Ug = np.asarray(U)[idx].reshape(len(idx), -1)
     err = np.abs(Ug - Uc).max(axis=1) / np.maximum(1.0, np.abs(Uc).max(axis=1))
-    return {
+    res = {
         "vs": "exact optimum (C restatement's polish, oracle/mpcqp_cpu.c); OSQP itself is absent, "
               "so parity with OSQP's own iterates is unpinned",
         "qps": int(len(idx)),
@@ -254,6 +254,16 @@ def spot_check(params, x0, ref, u_prev, U, active, status, idx) -> dict:
         "active_set_mismatches": int((np.asarray(active)[idx] != out["active"]).any(axis=1).sum()),
         "status_mismatches": int((np.asarray(status)[idx] != out["status"]).sum()),
     }
+    if iters is not None and len(idx):
+        # iteration indexing: the fraction of QPs whose four counters (ADMM iterations, polish passes,
+        # factorizations, line-search trials) equal the C restatement's; the fast kernel's wave-tree
+        # reductions round differently from the sequential sums (reproducible = 1 agrees on all)
+        it = np.asarray(iters)[idx]
+        same = it == out["iters"]
+        res["iters_agreement"] = float(same.all(axis=1).mean())
+        res["iters_agreement_per_counter"] = {k: float(same[:, i].mean()) for i, k in
+                                              enumerate(("admm", "polish", "factorizations", "ls_trials"))}
+    return res
 
 
 def cpu_baseline(params, x0, ref, u_prev, seconds: float) -> dict:
@@ -285,11 +295,11 @@ def cpu_baseline(params, x0, ref, u_prev, seconds: float) -> dict:
         "threads": threads,
         "host_cores_visible": visible,
         "value_1core": n1 / dt1,
-        "value_all_visible_cores_linear": n1 / dt1 * visible,
         "cpu_model": _cpu_model(),
         "sample": f"{done} QPs ({done // len(x0)} passes over this rank's batch) in {dt:.1f} s on {threads} "
-                  f"OpenMP threads ({visible} cores visible; the GPU box assigns OMP_NUM_THREADS per GPU), "
-                  f"C restatement of the same ADMM+polish algorithm (oracle/mpcqp_cpu.c)",
+                  f"OpenMP threads: the host's CPU share of this GPU (OMP_NUM_THREADS; {visible} cores are "
+                  f"visible to the process, shared with the node's other GPUs); C restatement of the same "
+                  f"ADMM+polish algorithm (oracle/mpcqp_cpu.c)",
     }
 
 
@@ -453,7 +463,8 @@ def main() -> int:
                        float(iters[:, 1].sum())])
     # end-of-run gather of the per-QP results (u0, status, U, active) to every rank
     g = {k: gather_rows(ctx, t[:B], counts) for k, t in
-         (("u0", ctrl._u0), ("status", ctrl._status), ("U", ctrl._U), ("active", ctrl._active))}
+         (("u0", ctrl._u0), ("status", ctrl._status), ("U", ctrl._U), ("active", ctrl._active),
+          ("iters", ctrl._iters))}
     g = {k: v.cpu().numpy() for k, v in g.items()}
 
     if rank == 0:
@@ -524,7 +535,7 @@ def main() -> int:
         if args.check_sample > 0:
             idx = np.unique(np.linspace(0, total - 1, min(total, args.check_sample)).astype(int))
             out["rel_err"] = spot_check(params, batch.x0, batch.ref, batch.u_prev, g["U"], g["active"],
-                                        g["status"], idx)
+                                        g["status"], idx, g["iters"])
             out["rel_err"]["gathered_qps"] = int(len(g["status"]))
             out["rel_err"]["gathered_solved"] = int((g["status"] == 1).sum())
         if world == 1 and args.cpu_seconds > 0:
