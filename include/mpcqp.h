@@ -47,7 +47,10 @@ extern "C" {
 
 #define MPCQP_MAX_HORIZON 1024   /* per-QP workspace 16 (2N)^2 bytes: 67 MB at N = 1024 */
 #define MPCQP_WIDE_MIN_HORIZON 32 /* N <= 31: one wave per QP (2N variables on the lanes, the KKT
-                                     inverse in registers); N >= 32: one 256-thread workgroup per QP */
+                                     inverse in registers); N >= 32: one workgroup per QP */
+#define MPCQP_MID_MAX_HORIZON 63  /* 32 <= N <= 63 (fast mode): 4 x 1-2 waves per QP, the KKT inverse's
+                                     rows split in four column parts over their registers; beyond, and in
+                                     reproducible mode, 256 threads restating the C code */
 
 /* per-QP status codes (mirror OSQP's; mpc_controller.py:137 accepts 1 and 2) */
 #define MPCQP_SOLVED 1            /* polish converged: exact optimum (active set reproduces itself) */

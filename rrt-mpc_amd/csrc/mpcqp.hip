@@ -95,7 +95,20 @@ const mpcqp::launcher_t kLaunchers[MPCQP_WIDE_MIN_HORIZON] = {
 // per-QP doubles of the solver state buffer (debug state of the one-wave kernel, the workspace
 // of the long-horizon kernel)
 size_t ws_state_stride(int N, bool wide) {
-  return wide ? mpcqp::wide_stride(N) : (size_t)state_stride(N);
+  if (!wide) return (size_t)state_stride(N);
+  const size_t w = mpcqp::wide_stride(N);
+  const size_t m = N <= MPCQP_MID_MAX_HORIZON ? mpcqp::mid_stride(N) : 0;
+  return w > m ? w : m;
+}
+
+void launch_mid(hipStream_t s, const Launch& L) {
+  switch (mpcqp::mid_bucket(L.p->horizon)) {
+    case 32: mpcqp::launch_solve_mid<32>(s, L); break;
+    case 40: mpcqp::launch_solve_mid<40>(s, L); break;
+    case 48: mpcqp::launch_solve_mid<48>(s, L); break;
+    case 56: mpcqp::launch_solve_mid<56>(s, L); break;
+    default: mpcqp::launch_solve_mid<64>(s, L); break;
+  }
 }
 
 thread_local std::string g_err;
@@ -129,7 +142,9 @@ bool wide_solve(const mpcqp_params& p) { return p.horizon >= MPCQP_WIDE_FROM || 
 launcher_t launcher(const mpcqp_params& p) {
   const int horizon = p.horizon;
   if (horizon < 1 || horizon > MPCQP_MAX_HORIZON) return nullptr;
-  if (wide_solve(p)) return &launch_solve_wide;
+  // fast mode up to MPCQP_MID_MAX_HORIZON: the mid kernel; beyond it, and in reproducible mode, the
+  // workgroup kernel that restates the C code operation for operation
+  if (wide_solve(p)) return p.reproducible == 0 && horizon <= MPCQP_MID_MAX_HORIZON ? &launch_mid : &launch_solve_wide;
   return horizon < MPCQP_WIDE_MIN_HORIZON ? kLaunchers[horizon] : nullptr;
 }
 }  // namespace mpcqp

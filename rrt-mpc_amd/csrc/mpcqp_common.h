@@ -285,7 +285,14 @@ void launch_solve(hipStream_t s, const Launch& L);
 // per QP, L.state = its workspace (wide_stride(N) doubles per QP)
 void launch_solve_wide(hipStream_t s, const Launch& L);
 size_t wide_stride(int horizon);
-// the solve of this parameter block runs the workgroup-per-QP kernel (long horizon or reproducible)
+// the mid-horizon fast solve (MPCQP_WIDE_MIN_HORIZON <= N <= MPCQP_MID_MAX_HORIZON, mpcqp_mid.hip):
+// one workgroup of 4 x (1 or 2) waves per QP, instantiated per padded horizon bucket NT; L.state = its
+// workspace (mid_stride(N) doubles per QP: the scaled Hessian)
+template <int NT>
+void launch_solve_mid(hipStream_t s, const Launch& L);
+inline int mid_bucket(int N) { return N <= 32 ? 32 : (N <= 40 ? 40 : (N <= 48 ? 48 : (N <= 56 ? 56 : 64))); }
+inline size_t mid_stride(int N) { return (size_t)2 * mid_bucket(N) * 128; }
+// the solve of this parameter block runs a workgroup-per-QP kernel (long horizon or reproducible)
 bool wide_solve(const mpcqp_params& p);
 // launcher of the parameter block's horizon / kernel (nullptr when not compiled in); defined in mpcqp.hip
 launcher_t launcher(const mpcqp_params& p);
