@@ -1,9 +1,9 @@
 // mpcqp_mid.hip -- the fast solve for mid horizons, MPCQP_WIDE_MIN_HORIZON <= N <= MPCQP_MID_MAX_HORIZON.
 //
 // The one-wave kernel (mpcqp_solve.h) keeps a QP's KKT inverse one row per lane, which caps it at
-// 2N <= 62 variables.  Here a QP owns one workgroup of 4 x R waves (R = 1 or 2 "row waves"): row i
-// of the KKT inverse (i = 64 wp + lane, padded to NP = 2 NT rows) is split into four column parts
-// h = 0..3 of CW = NP / 4 doubles each, held in the registers of waves (h, wp).  The h = 0 waves also own
+// 2N <= 62 variables.  Here a QP owns one workgroup of P x R waves (R = 1 or 2 "row waves"): row i
+// of the KKT inverse (i = 64 wp + lane, padded to NP = 2 NT rows) is split into P = 2 or 4 column parts
+// h of CW = NP / P doubles each, held in the registers of waves (h, wp).  The h = 0 waves also own
 // the QP's per-variable data (one decision variable per row, as in the one-wave kernel: the speed
 // form W = (v_1, delta_0, v_2, ...), the banded soft rows, OSQP's scaling).  Dense products read
 // their operand from LDS (broadcast reads) and add the parts' partial sums through LDS; the
@@ -24,6 +24,29 @@ namespace {
 using mpcqp::Launch;
 
 constexpr int kMidLD = 128;  // row stride (doubles) of the workspace Pbar
+// Diagnostic builds only (-DMPCQP_MID_STAMPS, never the measured library): per-phase s_memtime sums of
+// each QP's thread 0, added into g_mid_stamps[] at the end (read by mpcqp_debug_mid_stamps_<NT>).
+#ifdef MPCQP_MID_STAMPS
+__device__ unsigned long long g_mid_stamps[16];
+struct MidStamps {
+  unsigned long long acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  unsigned long long t = 0;
+  __device__ __forceinline__ void begin() { t = __builtin_amdgcn_s_memtime(); }
+  __device__ __forceinline__ void end(int k) { acc[k] += __builtin_amdgcn_s_memtime() - t; }
+  __device__ __forceinline__ void flush() {
+    if (threadIdx.x == 0) {
+      for (int k = 0; k < 8; ++k) atomicAdd(&g_mid_stamps[k], acc[k]);
+      atomicAdd(&g_mid_stamps[8], 1ull);
+    }
+  }
+};
+#else
+struct MidStamps {
+  __device__ __forceinline__ void begin() {}
+  __device__ __forceinline__ void end(int) {}
+  __device__ __forceinline__ void flush() {}
+};
+#endif
 #ifndef MPCQP_MID_WAVES  // waves per SIMD the register allocation targets
 #define MPCQP_MID_WAVES 2
 #endif
@@ -31,7 +54,7 @@ constexpr int kMidLD = 128;  // row stride (doubles) of the workspace Pbar
 // f(c, ld(c)) for c in [0, NT), the loads issued one group of G ahead of their uses and no further
 // (a scheduling barrier per group): the operand column never occupies more than 2 G registers next to
 // the NT doubles of the row (hoisting every load ahead of the FMAs spills the row).
-template <int NT, int G = 8, class Ld, class F>
+template <int NT, int G = 4, class Ld, class F>
 __device__ __forceinline__ void piped(Ld&& ld, F&& f) {
   double cur[G], nxt[G];
   Unroll<0, G>::run([&](auto kc) {
@@ -60,7 +83,9 @@ struct MidShape {
   static constexpr int NP = 2 * NT;                          // padded decision variables
   static constexpr int kRW = (NP + kWave - 1) / kWave;       // row waves (1 or 2)
   static constexpr int kNX = kRW * kWave;                    // rows covered
-  static constexpr int kParts = 4;                           // column parts of a row
+  // column parts of a row: 2 up to NT = 48 (the row part fits the registers of 2 waves per SIMD next to
+  // the rest, and a workgroup of 2 or 4 waves leaves room for two per CU), 4 beyond
+  static constexpr int kParts = NT <= 48 ? 2 : 4;
   static constexpr int CW = NP / kParts;                     // columns per part (even)
   static constexpr int kWaves = kParts * kRW;
   static constexpr int kThreads = kWaves * kWave;
@@ -80,13 +105,15 @@ struct MidLds {
   double band[5][X];            // form(): band entries (i, i - 4 .. i + 4) per row
   double cf[6][X];              // Cbar coefficients per variable (rank-1 rows)
   double dw[3][X];              // polish: soft-row weight changes since the last factorization
+  double blo[3][X], bhi[3][X], bwb[3][X], bE[3][X];  // per variable: scaled soft-row bounds, weights,
+                                                     // row scalings (LDS, not registers: see Mid)
   double red[2][8][8];          // cross-wave reductions (two slots, up to 8 values, 8 waves)
   unsigned long long msk[2][3][2];  // changed-row ballots of the row waves (two slots)
   double model[model_stride(NT)];
   double pre[4][NT + 1];
   double err[NT + 1][4];
-  double g[S::NP + 2];
-  double W[S::NP + 2];
+  double g[S::kNX + 2];
+  double W[S::kNX + 2];
 };
 
 template <int NT>
@@ -102,10 +129,17 @@ struct Mid {
   bool V, act, even;
   int xs, rs;  // exchange / reduction slot toggles (uniform)
   double dt, D, qv, cscale;
-  double E[3], lo[3], hi[3], wb[3];
+  // the soft rows' bounds / weights / row scalings live in LDS (read per use through the opaque row
+  // index, so they are not hoisted into registers): 24 VGPRs the register budget needs elsewhere
+  __device__ __forceinline__ double LO(int k) const { return sm->blo[k][i]; }
+  __device__ __forceinline__ double HI(int k) const { return sm->bhi[k][i]; }
+  __device__ __forceinline__ double WB(int k) const { return sm->bwb[k][i]; }
+  __device__ __forceinline__ double EE(int k) const { return sm->bE[k][i]; }
   double c0, c10, c11, c20, c21, c22;
   double r[CW];  // KKT (inverse) row i, columns [h CW, h CW + CW): A^{-1}[i][j] = -r
   int n_full, n_r1;
+  MidStamps T;  // phases: 0 setup, 1 ADMM factorizations, 2 ADMM iterations, 3 termination checks,
+                // 4 polish factorizations / rank-1 updates, 5 polish rest, 6 outputs, 7 whole QP
 
   __device__ __forceinline__ static void sync() { __syncthreads(); }
 
@@ -113,11 +147,7 @@ struct Mid {
   __device__ __forceinline__ void opaque() {
     asm volatile("" : "+v"(i));
     asm volatile("" : "+v"(D), "+v"(qv));
-    asm volatile("" : "+v"(E[0]), "+v"(E[1]), "+v"(E[2]));
     asm volatile("" : "+v"(c0), "+v"(c10), "+v"(c11), "+v"(c20), "+v"(c21), "+v"(c22));
-    asm volatile("" : "+v"(lo[0]), "+v"(lo[1]), "+v"(lo[2]));
-    asm volatile("" : "+v"(hi[0]), "+v"(hi[1]), "+v"(hi[2]));
-    asm volatile("" : "+v"(wb[0]), "+v"(wb[1]), "+v"(wb[2]));
   }
 
   // ---- cross-row-wave primitives (every thread of the workgroup calls them: they synchronize)
@@ -126,7 +156,7 @@ struct Mid {
   template <int Q>
   __device__ __forceinline__ void xchg(const double* v, double* m2, double* m4, double* p2, double* p4) {
     double(*e)[S::kNX + 8] = sm->ex[xs];
-    xs ^= 1;
+    xs = __builtin_amdgcn_readfirstlane(xs ^ 1);
     if (V)
 #pragma unroll
       for (int q = 0; q < Q; ++q) e[q][i + 4] = v[q];
@@ -144,7 +174,7 @@ struct Mid {
   template <int K, bool MAX>
   __device__ __forceinline__ void reduce(double* v) {
     double(*rd)[8] = sm->red[rs];
-    rs ^= 1;
+    rs = __builtin_amdgcn_readfirstlane(rs ^ 1);
 #pragma unroll
     for (int k = 0; k < K; ++k) {
       const double t = MAX ? wave_max(v[k]) : wave_sum(v[k]);
@@ -196,11 +226,16 @@ struct Mid {
     piped<CW>([&](auto c) { return b[c]; }, [&](auto c, double bc) { a[c % 4] = fma(r[c], bc, a[c % 4]); });
     return combine((a[0] + a[1]) + (a[2] + a[3]));
   }
-  // the parts' partial sums of row i added on the V thread: (s0 + s1) + (s2 + s3)
+  // the parts' partial sums of row i added on the V thread: s0 + s1, or (s0 + s1) + (s2 + s3)
   __device__ __forceinline__ double combine(double s) {
     if (!V) sm->pp[h - 1][i] = s;
     sync();
-    if (V) s = (s + sm->pp[0][i]) + (sm->pp[1][i] + sm->pp[2][i]);
+    if (V) {
+      if constexpr (kP == 2)
+        s = s + sm->pp[0][i];
+      else
+        s = (s + sm->pp[0][i]) + (sm->pp[1][i] + sm->pp[2][i]);
+    }
     return V && act ? s : 0.0;
   }
   __device__ __forceinline__ double inv_mul(double v) { return -kmul(v); }
@@ -354,7 +389,12 @@ struct Mid {
     if (V) {  // each term comes from one part (the others hold exact zeros): the one-wave order
       double t[3];
 #pragma unroll
-      for (int a = 0; a < 3; ++a) t[a] = (sm->tr[0][a][i] + sm->tr[1][a][i]) + (sm->tr[2][a][i] + sm->tr[3][a][i]);
+      for (int a = 0; a < 3; ++a) {
+        if constexpr (kP == 2)
+          t[a] = sm->tr[0][a][i] + sm->tr[1][a][i];
+        else
+          t[a] = (sm->tr[0][a][i] + sm->tr[1][a][i]) + (sm->tr[2][a][i] + sm->tr[3][a][i]);
+      }
       const double u = (t[0] + t[1]) + t[2];
       sm->vec[i] = act ? -u : 0.0;
     }
@@ -555,7 +595,12 @@ __device__ __forceinline__ bool mid_setup(const mpcqp_params& p, Mid<NT>& C) {
     double v = fmax(fmax(cm4[0], cm4[1]), fmax(cm4[2], cm4[3]));
     if (!V) sm.pp[C.h - 1][i] = v;
     __syncthreads();
-    if (V) v = fmax(fmax(v, sm.pp[0][i]), fmax(sm.pp[1][i], sm.pp[2][i]));
+    if (V) {
+      if constexpr (S::kParts == 2)
+        v = fmax(v, sm.pp[0][i]);
+      else
+        v = fmax(fmax(v, sm.pp[0][i]), fmax(sm.pp[1][i], sm.pp[2][i]));
+    }
     __syncthreads();
     return V && act ? v : 0.0;
   };
@@ -670,13 +715,14 @@ __device__ __forceinline__ bool mid_setup(const mpcqp_params& p, Mid<NT>& C) {
     C.c20 = (E[2] * k2[0]) * D;
     C.c21 = (E[2] * k2[1]) * Dm2;
     C.c22 = (E[2] * k2[2]) * Dm4;
+    if (V)
 #pragma unroll
-    for (int k = 0; k < 3; ++k) {
-      C.E[k] = E[k];
-      C.lo[k] = lo[k];
-      C.hi[k] = hi[k];
-      C.wb[k] = wb[k];
-    }
+      for (int k = 0; k < 3; ++k) {
+        sm.bE[k][i] = E[k];
+        sm.blo[k][i] = lo[k];
+        sm.bhi[k][i] = hi[k];
+        sm.bwb[k][i] = wb[k];
+      }
     if (V) {
       sm.cf[0][i] = C.c0;
       sm.cf[1][i] = C.c10;
@@ -701,7 +747,7 @@ __device__ __forceinline__ int mid_polish(Mid<NT>& C, double& x, const double zg
   C.Cmul(x, zc);
   double Px = C.Pmul(x);
 #pragma unroll
-  for (int k = 0; k < 3; ++k) cd[k] = zg[k] > C.hi[k] ? 2 : (zg[k] < C.lo[k] ? 1 : 0);
+  for (int k = 0; k < 3; ++k) cd[k] = zg[k] > C.HI(k) ? 2 : (zg[k] < C.LO(k) ? 1 : 0);
   const int kMaxRank1 = C.n / 2;
   double rwf[3] = {0.0, 0.0, 0.0};
   bool have_fact = false;
@@ -711,14 +757,14 @@ __device__ __forceinline__ int mid_polish(Mid<NT>& C, double& x, const double zg
     double rw[3], tmp[3];
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
-      rw[k] = cd[k] ? 2.0 * C.wb[k] : 0.0;
-      tmp[k] = cd[k] == 2 ? rw[k] * C.hi[k] : (cd[k] == 1 ? rw[k] * C.lo[k] : 0.0);
+      rw[k] = cd[k] ? 2.0 * C.WB(k) : 0.0;
+      tmp[k] = cd[k] == 2 ? rw[k] * C.HI(k) : (cd[k] == 1 ? rw[k] * C.LO(k) : 0.0);
     }
     bool refac = !have_fact;
     if (!refac) {
       // changed soft rows: each row wave's ballots, combined through LDS (uniform in every thread)
       unsigned long long(*mk)[2] = C.sm->msk[C.rs];
-      C.rs ^= 1;
+      C.rs = __builtin_amdgcn_readfirstlane(C.rs ^ 1);
 #pragma unroll
       for (int k = 0; k < 3; ++k) {
         const unsigned long long b = __ballot(act && rw[k] != rwf[k]);
@@ -750,8 +796,10 @@ __device__ __forceinline__ int mid_polish(Mid<NT>& C, double& x, const double zg
         }
     }
     if (refac) {
+      C.T.begin();
       C.form(0.0, rw);
       const bool okf = C.sweep();
+      C.T.end(4);
       ++C.n_full;
       if (C.bany(!okf)) {
         result = -1;
@@ -769,7 +817,7 @@ __device__ __forceinline__ int mid_polish(Mid<NT>& C, double& x, const double zg
     bool diff = false;
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
-      const int c2 = zn[k] > C.hi[k] ? 2 : (zn[k] < C.lo[k] ? 1 : 0);
+      const int c2 = zn[k] > C.HI(k) ? 2 : (zn[k] < C.LO(k) ? 1 : 0);
       diff = diff || (c2 != cd[k]);
     }
     if (C.bany(!isfinite(xn))) {
@@ -786,7 +834,7 @@ __device__ __forceinline__ int mid_polish(Mid<NT>& C, double& x, const double zg
       diff = false;
 #pragma unroll
       for (int k = 0; k < 3; ++k) {
-        const int c2 = zn[k] > C.hi[k] ? 2 : (zn[k] < C.lo[k] ? 1 : 0);
+        const int c2 = zn[k] > C.HI(k) ? 2 : (zn[k] < C.LO(k) ? 1 : 0);
         diff = diff || (c2 != cd[k]);
       }
       if (C.bany(!isfinite(xn))) {
@@ -802,7 +850,7 @@ __device__ __forceinline__ int mid_polish(Mid<NT>& C, double& x, const double zg
     // exact line search along d = xn - x
     double tb[3];
 #pragma unroll
-    for (int k = 0; k < 3; ++k) tb[k] = rw[k] * (zn[k] - (cd[k] == 2 ? C.hi[k] : (cd[k] == 1 ? C.lo[k] : 0.0)));
+    for (int k = 0; k < 3; ++k) tb[k] = rw[k] * (zn[k] - (cd[k] == 2 ? C.HI(k) : (cd[k] == 1 ? C.LO(k) : 0.0)));
     const double ctb = C.CTmul(tb);
     const double dx = act ? xn - x : 0.0;
     const double Pd = act ? (-ctb - C.qv) - Px : 0.0;
@@ -819,9 +867,9 @@ __device__ __forceinline__ int mid_polish(Mid<NT>& C, double& x, const double zg
 #pragma unroll
       for (int k = 0; k < 3; ++k) {
         const double zt = zc[k] + t * zd[k];
-        const double rr = zt > C.hi[k] ? zt - C.hi[k] : (zt < C.lo[k] ? zt - C.lo[k] : 0.0);
-        g12[0] += 2.0 * C.wb[k] * rr * zd[k];
-        if (rr != 0.0) g12[1] += 2.0 * C.wb[k] * zd[k] * zd[k];
+        const double rr = zt > C.HI(k) ? zt - C.HI(k) : (zt < C.LO(k) ? zt - C.LO(k) : 0.0);
+        g12[0] += 2.0 * C.WB(k) * rr * zd[k];
+        if (rr != 0.0) g12[1] += 2.0 * C.WB(k) * zd[k] * zd[k];
       }
       if (!C.V) g12[0] = g12[1] = 0.0;
       C.template reduce<2, false>(g12);
@@ -834,8 +882,8 @@ __device__ __forceinline__ int mid_polish(Mid<NT>& C, double& x, const double zg
 #pragma unroll
       for (int k = 0; k < 3; ++k) {
         const double za = zc[k] + t * zd[k], zb = zc[k] + tn * zd[k];
-        const int ca = za > C.hi[k] ? 2 : (za < C.lo[k] ? 1 : 0);
-        const int cb = zb > C.hi[k] ? 2 : (zb < C.lo[k] ? 1 : 0);
+        const int ca = za > C.HI(k) ? 2 : (za < C.LO(k) ? 1 : 0);
+        const int cb = zb > C.HI(k) ? 2 : (zb < C.LO(k) ? 1 : 0);
         moved = moved || ca != cb;
       }
       t = tn;
@@ -845,7 +893,7 @@ __device__ __forceinline__ int mid_polish(Mid<NT>& C, double& x, const double zg
     Px = Px + t * Pd;
     C.Cmul(x, zc);
 #pragma unroll
-    for (int k = 0; k < 3; ++k) cd[k] = zc[k] > C.hi[k] ? 2 : (zc[k] < C.lo[k] ? 1 : 0);
+    for (int k = 0; k < 3; ++k) cd[k] = zc[k] > C.HI(k) ? 2 : (zc[k] < C.LO(k) ? 1 : 0);
   }
   return result;
 }
@@ -868,9 +916,11 @@ __device__ __forceinline__ int mid_admm(const mpcqp_params& p, Mid<NT>& C, MidAd
   while (S.it < p.max_iter && !done) {
     if (S.need_fact) {
       const double rw[3] = {S.rho, S.rho, S.rho};
+      C.T.begin();
       C.form(sg, rw);
       ++S.nfact;
       const bool okf = C.sweep();
+      C.T.end(1);
       if (C.bany(!okf)) {
         ev = kMidBad;
         break;
@@ -881,13 +931,14 @@ __device__ __forceinline__ int mid_admm(const mpcqp_params& p, Mid<NT>& C, MidAd
     double pb[3], rpb[3];
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
-      pb[k] = 2.0 * C.wb[k] / (rho + 2.0 * C.wb[k]);
+      pb[k] = 2.0 * C.WB(k) / (rho + 2.0 * C.WB(k));
       rpb[k] = rho * pb[k];
     }
     const double ir = 1.0 / rho, oma = 1.0 - alpha;
     while (!S.need_fact && S.it < p.max_iter) {
       const int it = ++S.it;
       C.opaque();
+      C.T.begin();
       double tmp[3];
 #pragma unroll
       for (int k = 0; k < 3; ++k) tmp[k] = rho * S.z[k] - S.y[k];
@@ -900,19 +951,21 @@ __device__ __forceinline__ int mid_admm(const mpcqp_params& p, Mid<NT>& C, MidAd
       for (int k = 0; k < 3; ++k) {
         const double v = za[k] + oma * S.z[k];
         const double vv = v + S.y[k] * ir;
-        const double d = vv - min_nc(max_nc(vv, C.lo[k]), C.hi[k]);
+        const double d = vv - min_nc(max_nc(vv, C.LO(k)), C.HI(k));
         S.z[k] = vv - pb[k] * d;
         S.y[k] = rpb[k] * d;
       }
+      C.T.end(2);
       if (it % p.check_termination == 0 || it == p.max_iter) {
+        C.T.begin();
         const double x = S.x;
         double Ax[3];
         C.Cmul(x, Ax);
         double mx[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // pr nprim spr snprim du ndual sdu sndual
 #pragma unroll
         for (int k = 0; k < 3; ++k) {
-          if (C.E[k] > 0.0) {
-            const double ie = 1.0 / C.E[k];
+          if (C.EE(k) > 0.0) {
+            const double ie = 1.0 / C.EE(k);
             mx[0] = fmax(mx[0], fabs((Ax[k] - S.z[k]) * ie));
             mx[1] = fmax(mx[1], fmax(fabs(Ax[k] * ie), fabs(S.z[k] * ie)));
             mx[2] = fmax(mx[2], fabs(Ax[k] - S.z[k]));
@@ -942,6 +995,7 @@ __device__ __forceinline__ int mid_admm(const mpcqp_params& p, Mid<NT>& C, MidAd
         du *= ic;
         const double ep = p.eps_abs + p.eps_rel * nprim;
         const double ed = p.eps_abs + p.eps_rel * ndual * ic;
+        C.T.end(3);
         if (nf || !isfinite(pr) || !isfinite(du)) {
           ev = kMidBad;
           done = true;
@@ -1051,7 +1105,10 @@ __device__ __forceinline__ void mid_finish(const mpcqp_params& p, int b, Mid<NT>
     }
     // psi_{k+1} = x02 + sum_{j <= k} si_j delta_j (the one-wave kernel's scan over the steering lanes)
     const double sacc = scan_add(k < N ? m_si * dl : 0.0, k);
-    const double pk = k == 0 ? x02 : x02 + dpp<kWaveShr1>(sacc);
+    // the shift with every lane active (pinned: sunk into the k != 0 branch, lane 0 would read as 0)
+    double psh = dpp<kWaveShr1>(sacc);
+    asm volatile("" : "+v"(psh));
+    const double pk = k == 0 ? x02 : x02 + psh;
     const double vk = k == 0 ? x03 : (k <= N ? sm.W[2 * (k - 1)] : 0.0);
     double t0 = 0.0, t1 = 0.0;
     if (k < N) {
@@ -1118,7 +1175,11 @@ __global__ __launch_bounds__(MidShape<NT>::kThreads, MPCQP_MID_WAVES) void k_sol
   const double* mb = model + (size_t)b * model_stride(N);
   for (int e = tid; e < model_stride(N); e += S::kThreads) sm.model[e] = mb[e];
   __syncthreads();
+  MidStamps TQ;
+  TQ.begin();
+  C.T.begin();
   bool bad = mid_setup<NT>(p, C);
+  C.T.end(0);
   const bool use_admm = p.method == MPCQP_METHOD_ADMM;
   MidAdmm A;
   A.x = 0.0;
@@ -1155,8 +1216,14 @@ __global__ __launch_bounds__(MidShape<NT>::kThreads, MPCQP_MID_WAVES) void k_sol
     }
     if (kind == 0) break;
     double xp = kind == 1 ? A.x : x;
+    MidStamps TP;
+    TP.begin();
     const int r_ = mid_polish<NT>(C, xp, zg, kind == 1 ? p.polish_attempt_max_iter : p.polish_max_iter, pol_it,
                                   A.nfact, n_ls);
+    TP.end(0);
+#ifdef MPCQP_MID_STAMPS
+    C.T.acc[5] += TP.acc[0];
+#endif
     if (kind == 2) {
       x = xp;
       bad = r_ < 0;
@@ -1174,8 +1241,15 @@ __global__ __launch_bounds__(MidShape<NT>::kThreads, MPCQP_MID_WAVES) void k_sol
     if (A.rho_change) A.rho = A.rho_next;
     A.rho_change = false;
   }
+  C.T.begin();
   mid_finish<NT>(p, b, C, x, x_admm, flag, do_polish, pol_ok, bad, A.it, A.nfact, pol_it, n_ls, u0o, Xo, Uo,
                  statuso, iterso, activeo);
+  C.T.end(6);
+  TQ.end(0);
+#ifdef MPCQP_MID_STAMPS
+  C.T.acc[7] += TQ.acc[0];
+#endif
+  C.T.flush();
 }
 
 }  // namespace
@@ -1192,3 +1266,17 @@ void launch_solve_mid(hipStream_t s, const Launch& L) {
 #endif
 template void launch_solve_mid<MPCQP_MID_PART>(hipStream_t, const Launch&);
 }  // namespace mpcqp
+
+#ifdef MPCQP_MID_STAMPS
+#define MPCQP_CAT2(a, b) a##b
+#define MPCQP_CAT(a, b) MPCQP_CAT2(a, b)
+extern "C" int MPCQP_CAT(mpcqp_debug_mid_stamps_, MPCQP_MID_PART)(unsigned long long* out16, int reset) {
+  hipError_t e = hipDeviceSynchronize();
+  if (e == hipSuccess && out16) e = hipMemcpyFromSymbol(out16, HIP_SYMBOL(g_mid_stamps), sizeof(unsigned long long) * 16);
+  if (e == hipSuccess && reset) {
+    unsigned long long z[16] = {0};
+    e = hipMemcpyToSymbol(HIP_SYMBOL(g_mid_stamps), z, sizeof(z));
+  }
+  return e == hipSuccess ? 0 : -4;
+}
+#endif
