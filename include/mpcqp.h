@@ -269,6 +269,16 @@ int mpcqp_rrt_plan(const mpcqp_rrt_params* p, int V, const uint8_t* occupancy, c
                    void* stream);
 
 /*
+ * The planner's elementary functions over n device values, as the RRT* kernels evaluate them
+ * (csrc/mpcqp_math.h) -- exposed so tests can hold them to the host's bit for bit:
+ *   op 0  out0 = math.hypot(a, b) as CPython computes it (rrt_star.py:319, :362-363)
+ *   op 1  _steer (rrt_star.py:307-311): out0 = atan2(a, b) (a = dy, b = dx), out1 = cos(out0),
+ *         out2 = sin(out0), each correctly rounded (glibc's agree on ~99.9 % of arguments)
+ */
+int mpcqp_plan_math(int op, int n, const double* a, const double* b, double* out0, double* out1, double* out2,
+                    void* stream);
+
+/*
  * Path extraction + shortcut pruning for the trees mpcqp_rrt_plan grew (replaces the host
  * post-processing of src/planning/rrt_star.py:245-262 and _shortcut_prune :376-389; the
  * Catmull-Rom smoothing :264-283 stays with the caller).  Same params, occupancy and

@@ -4,6 +4,7 @@
 // swarm (mpcqp_swarm.hip).
 #pragma once
 #include "mpcqp_common.h"
+#include "mpcqp_math.h"
 
 namespace {
 
@@ -23,7 +24,7 @@ struct Grid {
 __device__ bool segment_free(const Grid& g, double ax, double ay, double bx, double by, int i0, int stride) {
 #pragma clang fp contract(off)
   const double dx = bx - ax, dy = by - ay;
-  const double dist = hypot(dx, dy);
+  const double dist = mpcqp_math::py_hypot(dx, dy);
   const double st = fmax(g.cstep, 1e-3);
   const int n = max(1, (int)ceil(dist / st));
   const double sx = dx / n, sy = dy / n;
@@ -179,7 +180,7 @@ __device__ void rrt_grow_one(const mpcqp_rrt_params& p, const uint8_t* __restric
     double bd = INFINITY;
     int bi = 0x7fffffff;
     for (int i = tid; i < count; i += kPlanThreads) {
-      const double d = hypot(X[i] - qx, Y[i] - qy);
+      const double d = mpcqp_math::py_hypot(X[i] - qx, Y[i] - qy);
       if (d < bd) {
         bd = d;
         bi = i;
@@ -188,17 +189,19 @@ __device__ void rrt_grow_one(const mpcqp_rrt_params& p, const uint8_t* __restric
     block_argmin(bd, bi, sm);
     const int near = bi;
     const double fx = X[near], fy = Y[near];
-    const double th = atan2(qy - fy, qx - fx);
-    const double nx = fx + p.step * cos(th);
-    const double ny = fy + p.step * sin(th);
+    // _steer (rrt_star.py:307-311): math.atan2 / cos / sin, correctly rounded (mpcqp_math.h)
+    double th, cth, sth;
+    mpcqp_math::cr_steer(qy - fy, qx - fx, th, cth, sth);
+    const double nx = fx + p.step * cth;
+    const double ny = fy + p.step * sth;
     if (!(0.0 <= nx && nx < (double)p.width && 0.0 <= ny && ny < (double)p.height)) continue;
     if (!block_all(segment_free(g, fx, fy, nx, ny, tid, kPlanThreads), sm)) continue;
     // choose parent
-    const double c0 = C[near] + hypot(fx - nx, fy - ny);
+    const double c0 = C[near] + mpcqp_math::py_hypot(fx - nx, fy - ny);
     double bc = INFINITY;
     int bp = 0x7fffffff;
     for (int i = tid; i < count; i += kPlanThreads) {
-      const double d = hypot(X[i] - nx, Y[i] - ny);
+      const double d = mpcqp_math::py_hypot(X[i] - nx, Y[i] - ny);
       if (d > p.rewire_radius) continue;
       if (!segment_free(g, X[i], Y[i], nx, ny, 0, 1)) continue;
       const double c = C[i] + d;
@@ -222,7 +225,7 @@ __device__ void rrt_grow_one(const mpcqp_rrt_params& p, const uint8_t* __restric
     count = ni + 1;
     // rewire (every node updated at most once, from its own pre-rewire values)
     for (int i = tid; i < ni; i += kPlanThreads) {
-      const double d = hypot(X[i] - nx, Y[i] - ny);
+      const double d = mpcqp_math::py_hypot(X[i] - nx, Y[i] - ny);
       if (d > p.rewire_radius) continue;
       if (Par[i] < 0) continue;
       const double c = cost + d;
@@ -233,12 +236,12 @@ __device__ void rrt_grow_one(const mpcqp_rrt_params& p, const uint8_t* __restric
     }
     __syncthreads();
     // goal
-    if (hypot(nx - gx, ny - gy) < p.goal_radius) {
+    if (mpcqp_math::py_hypot(nx - gx, ny - gy) < p.goal_radius) {
       if (!block_all(segment_free(g, nx, ny, gx, gy, tid, kPlanThreads), sm)) continue;
       if (tid == 0) {
         X[count] = gx;
         Y[count] = gy;
-        C[count] = cost + hypot(nx - gx, ny - gy);
+        C[count] = cost + mpcqp_math::py_hypot(nx - gx, ny - gy);
         Par[count] = ni;
       }
       goal_index = count;

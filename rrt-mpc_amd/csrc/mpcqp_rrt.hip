@@ -58,9 +58,39 @@ __global__ __launch_bounds__(kPlanThreads) void k_rrt_paths(mpcqp_rrt_params p, 
                   raw_len + v, pruned + (size_t)v * M * 2, pruned_len + v, lds, sm);
 }
 
+// The planner's elementary functions over arrays (mpcqp_plan_math): the values the RRT* kernels use.
+__global__ __launch_bounds__(256) void k_plan_math(int op, int n, const double* __restrict__ a,
+                                                    const double* __restrict__ b, double* __restrict__ o0,
+                                                    double* __restrict__ o1, double* __restrict__ o2) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  if (op == 0) {
+    o0[i] = mpcqp_math::py_hypot(a[i], b[i]);
+  } else {
+    double th, c, s;
+    mpcqp_math::cr_steer(a[i], b[i], th, c, s);
+    o0[i] = th;
+    o1[i] = c;
+    o2[i] = s;
+  }
+}
+
 }  // namespace
 
 extern "C" {
+
+int mpcqp_plan_math(int op, int n, const double* a, const double* b, double* out0, double* out1, double* out2,
+                    void* stream) {
+  if (op != 0 && op != 1) return fail(MPCQP_E_ARG, "op must be 0 (hypot) or 1 (steer)");
+  if (n < 0) return fail(MPCQP_E_ARG, "n must be >= 0");
+  if (n == 0) return MPCQP_OK;
+  if (!a || !b || !out0 || (op == 1 && (!out1 || !out2))) return fail(MPCQP_E_ARG, "null argument");
+  hipLaunchKernelGGL(k_plan_math, dim3((n + 255) / 256), dim3(256), 0, static_cast<hipStream_t>(stream), op, n, a, b,
+                     out0, out1, out2);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return fail(MPCQP_E_HIP, std::string("k_plan_math launch: ") + hipGetErrorString(e));
+  return MPCQP_OK;
+}
 
 int mpcqp_rrt_paths(const mpcqp_rrt_params* p, int V, int prune, const uint8_t* occupancy, const double* nodes,
                     const int32_t* count, const int32_t* meta, double* raw, int32_t* raw_len, double* pruned,

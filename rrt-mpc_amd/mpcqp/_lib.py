@@ -237,6 +237,7 @@ _SYMBOLS = {
     "mpcqp_rrt_paths": ([ctypes.POINTER(MpcqpRrtParams), ctypes.c_int, ctypes.c_int] + [ctypes.c_void_p] * 9,
                         ctypes.c_int),
     "mpcqp_inflate": ([ctypes.c_int] * 4 + [ctypes.c_void_p] * 3, ctypes.c_int),
+    "mpcqp_plan_math": ([ctypes.c_int, ctypes.c_int] + [ctypes.c_void_p] * 6, ctypes.c_int),
     "mpcqp_catmull_rom": ([ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_double,
                            ctypes.c_double, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p],
                           ctypes.c_int),

@@ -87,10 +87,11 @@ def _host_continue(state, u_prev, path, goal, steps):
     return np.asarray(mo.track_from(_oracle_params(), ref, state, u_prev, goal, steps, solve_fn=_c_solve))
 
 
-def _oracle_plan(occ, start, goal, seed):
+def _oracle_plan(occ, start, goal, seed, cr=False):
     """RRTStarPlanner.plan (rrt_star.py:201-283) on the host: oracle/rrt_oracle.grow_tree fed the
     seed's own sample stream (draw_samples), oracle extraction and shortcut pruning, then the
-    Catmull-Rom smoothing of the host restatement (pinned by branches.npz)."""
+    Catmull-Rom smoothing of the host restatement (pinned by branches.npz).  cr: the steer's
+    trig correctly rounded (the device's) instead of glibc's."""
     import rrt_oracle as ro
     from mpcqp.common.geometry import catmull_rom_spline
     from mpcqp.planning.rrt_star import draw_samples
@@ -98,7 +99,8 @@ def _oracle_plan(occ, start, goal, seed):
     prm = _planner_params(seed)
     smp = draw_samples(int(seed), goal, occ.shape, prm.goal_sample_rate, prm.max_iterations)
     nodes, _, gi = ro.grow_tree(occ, start, goal, smp, step=prm.step, goal_radius=prm.goal_radius,
-                                rewire_radius=prm.rewire_radius, collision_step=prm.collision_step)
+                                rewire_radius=prm.rewire_radius, collision_step=prm.collision_step,
+                                trig=ro.CR_TRIG if cr else ro.LIBM_TRIG)
     if gi < 0:
         return None
     path = ro.extract_path(nodes, gi)
@@ -116,13 +118,24 @@ def _oracle_plan(occ, start, goal, seed):
 
 def _check_plan(occ, start, goal, seed, path, tol=1e-4):
     """The device plan against the host restatement of the reference planner (_oracle_plan): same
-    number of points, coordinates within the ~1e-5 px the duplicated end knots amplify an ulp to."""
-    plan = _oracle_plan(occ, start, goal, seed)
+    number of points, coordinates within the ~1e-5 px the duplicated end knots amplify an ulp to
+    (the trees themselves are bit-exact, test_gpu_planning.py).  Where the plan differs from the
+    libm restatement's, it must be the plan with correctly rounded steer trig (glibc's rounding,
+    rare).  Returns "libm" or "cr"."""
+    got = np.asarray(path)
+
+    def same(plan):
+        return plan is not None and np.asarray(plan).shape == got.shape and \
+            np.abs(np.asarray(plan) - got).max() <= tol
+
+    if same(_oracle_plan(occ, start, goal, seed)):
+        return "libm"
+    plan = _oracle_plan(occ, start, goal, seed, cr=True)
     assert plan is not None
     ref = np.asarray(plan)
-    got = np.asarray(path)
     assert ref.shape == got.shape, (ref.shape, got.shape)
     np.testing.assert_allclose(got, ref, rtol=0, atol=tol)
+    return "cr"
 
 
 def test_device_smoothing_matches_reference_planner(cuda, golden):
@@ -202,8 +215,9 @@ def test_per_step_replan_100_vehicles(cuda, golden):
         host = _host_track(res.paths[v], starts[v], goals[v], steps)
         assert res.steps[v] == len(host), v
         np.testing.assert_allclose(res.states[v], host, rtol=0, atol=1e-7)
-    for v in np.flatnonzero(res.planned):  # every initial plan: the reference planner's, seed v
-        _check_plan(occ, starts[v], goals[v], v, res.paths[v])
+    kinds = [_check_plan(occ, starts[v], goals[v], v, res.paths[v])  # every initial plan: seed v
+             for v in np.flatnonzero(res.planned)]
+    assert kinds.count("cr") <= 2, kinds
     for v in ok_replans:
         s = int(res.replan_steps[v, 0])  # steps taken when the replan committed
         host = _host_track(res.paths[v], starts[v], goals[v], s)

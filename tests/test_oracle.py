@@ -229,6 +229,40 @@ def test_rrt_oracle_reproduces_reference_trees(golden):
         assert [int(g[f"rrt{k}_meta"][0]), it, gi] == [int(gi >= 0), *map(int, g[f"rrt{k}_meta"][1:])]
 
 
+def test_correctly_rounded_trig_oracle(golden):
+    """rrt_oracle.cr_*: the exact (decimal) correctly rounded steer trig.  Within an ulp of glibc's
+    and equal to it on >= 99 % of arguments; a rounding-error-free identity holds exactly; and the
+    reference's own trees (planning.npz) come out bit for bit the same with it -- the device's
+    trig (correctly rounded) can match the reference wherever glibc rounds correctly."""
+    import math
+
+    import rrt_oracle as ro
+    from mpcqp.planning.rrt_star import default_planner_parameters, draw_samples
+
+    rng = np.random.default_rng(4)
+    t = rng.uniform(-math.pi, math.pi, 3000)
+    for f, g in ((ro.cr_cos, math.cos), (ro.cr_sin, math.sin)):
+        a = np.array([f(v) for v in t])
+        b = np.array([g(v) for v in t])
+        assert (a == b).mean() >= 0.99
+        assert np.all(np.abs(a - b) <= np.spacing(np.abs(b)))
+    y, x = rng.uniform(-80, 80, (2, 3000))
+    a = np.array([ro.cr_atan2(p, q) for p, q in zip(y, x)])
+    b = np.array([math.atan2(p, q) for p, q in zip(y, x)])
+    assert (a == b).mean() >= 0.99 and np.all(np.abs(a - b) <= np.spacing(np.abs(b)))
+    assert ro.cr_atan2(1.0, 1.0) == math.pi / 4 and ro.cr_cos(0.0) == 1.0 and ro.cr_atan2(0.0, -1.0) == math.pi
+    g = golden("planning.npz")
+    occ = g["rrt_occupancy"]
+    prm = default_planner_parameters()
+    for k in range(5):
+        sx, sy, gx, gy, seed, iters = g[f"rrt{k}_case"]
+        smp = draw_samples(int(seed), (gx, gy), occ.shape, prm.goal_sample_rate, int(iters))
+        nodes, it, gi = ro.grow_tree(occ, (sx, sy), (gx, gy), smp, step=prm.step, goal_radius=prm.goal_radius,
+                                     rewire_radius=prm.rewire_radius, collision_step=prm.collision_step,
+                                     trig=ro.CR_TRIG)
+        np.testing.assert_array_equal(nodes, g[f"rrt{k}_nodes"])
+
+
 def test_inflation_oracle_reproduces_reference(golden):
     import rrt_oracle as ro
 
