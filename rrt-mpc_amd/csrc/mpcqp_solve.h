@@ -8,7 +8,18 @@ using mpcqp::Launch;
 // The model block stays in LDS for the outputs (finish_qp) while Pbar is live, where that costs no
 // occupancy (8 workgroups of Pbar + model fit a CU's 160 KB of LDS: N <= 23); past that, the model shares
 // the setup's union with Pbar and the outputs re-derive it (K1 fused) or re-read it (workspace).
+// Pbar storage.  N <= 23: row-major n x (n + 1) (column n: zero padding), lane `col` reads column
+// col (conflict-free).  N >= 24: the lower triangle packed (row a, column b <= a at a (a + 1) / 2 + b)
+// for 64 rows, rows n..63 zero: 16.6 KB instead of 32 N^2 bytes, so eight workgroups fit a CU's LDS
+// (the full matrix allowed 7 at N = 24, 5 from N = 28 on) and the kernel runs 2 waves per SIMD (Pbar is read only by form() and Pmul: a factorization or a
+// residual check, not per ADMM iteration).
+#ifndef MPCQP_PACKED_FROM
+#define MPCQP_PACKED_FROM 24
+#endif
 template <int N>
+constexpr bool kPackedP = N >= MPCQP_PACKED_FROM;
+
+template <int N, bool Packed = kPackedP<N>>
 struct SolveSmem {
   static constexpr int n = 2 * N;
   static constexpr int kPS = n + 1;  // row stride: column n is a zero padding column
@@ -17,6 +28,15 @@ struct SolveSmem {
   double pad1[4];     // zeros: ... and those of the last rows
   double band[5][n];  // Pbar's entries at form()'s band addresses (lane p: (p, p + 2d - 4)), restored after each form
 };
+template <int N>
+struct SolveSmem<N, true> {
+  static constexpr int n = 2 * N;
+  static constexpr int kPS = 0;  // unused
+  double P[kWave * (kWave + 1) / 2];  // lower triangle, packed by rows; rows >= n zero
+  double band[3][n];                  // Pbar's entries (p, p - 4), (p, p - 2), (p, p) (form() adds there)
+};
+// packed index of (i, j), i / j any order
+__device__ __forceinline__ int tri_idx(int i, int j) { return i >= j ? (i * (i + 1)) / 2 + j : (j * (j + 1)) / 2 + i; }
 
 template <int N>
 constexpr bool kModelKept =
@@ -128,7 +148,16 @@ struct Ctx {
     vbcast(act ? v : 0.0, w);
     const int col = act ? lane : n;  // lanes >= n read the zero padding column
     double a[4] = {0.0, 0.0, 0.0, 0.0};
-    if constexpr (N > 24) {
+    if constexpr (kPackedP<N>) {  // lanes >= n read their zero rows
+      int ln = lane;
+      asm volatile("" : "+v"(ln));
+      const int Ti = (ln * (ln + 1)) / 2;
+      Unroll<0, n>::run([&](auto jc) {
+        constexpr int j = decltype(jc)::value;
+        fmac_bc<j % 16>(a[j % 4], w[j / 16], P[ln >= j ? Ti + j : (j * (j + 1)) / 2 + ln]);
+      });
+      return act ? (a[0] + a[1]) + (a[2] + a[3]) : 0.0;
+    } else if constexpr (N > 24) {
       Unroll<0, n>::run([&](auto jc) {
         constexpr int j = decltype(jc)::value;
         fmac_bc<j % 16>(a[j % 4], w[j / 16], P[j * kPS + col]);
@@ -179,7 +208,35 @@ struct Ctx {
     const double bp4 = shl4(b2 * c20);                               // entry (p, p+4)
     const double bm2 = shr2(bp2), bm4 = shr4(bp4);  // symmetric: (p, p-2) = lane p-2's (., +2)
     const bool live = ln < n;
-    if constexpr (n >= 8) {
+    if constexpr (kPackedP<N>) {
+      // lower band entries only: lane p adds into (p, p - 4), (p, p - 2), (p, p); the upper ones
+      // (p, p + 2), (p, p + 4) are lanes p + 2 / p + 4's (p + 2, p), (p + 4, p) (the same words)
+      const int Ti = (ln * (ln + 1)) / 2;
+      double* rowp = P + Ti + ln;
+      const double* bo = band + ln;
+      lds_sync();
+      if (live) {
+        if (ln >= 4) rowp[-4] = bo[0 * n] + bm4;
+        if (ln >= 2) rowp[-2] = bo[1 * n] + bm2;
+        rowp[0] = bo[2 * n] + b0;
+      }
+      lds_sync();
+      Unroll<0, n>::run([&](auto jc) {  // lanes >= n read their zero rows
+        constexpr int j = decltype(jc)::value;
+        r[j] = P[ln >= j ? Ti + j : (j * (j + 1)) / 2 + ln];
+      });
+      lds_sync();
+      int l2 = lane;
+      asm volatile("" : "+v"(l2));
+      if (l2 < n) {
+        double* rp = P + (l2 * (l2 + 1)) / 2 + l2;
+        const double* bp = band + l2;
+        if (l2 >= 4) rp[-4] = bp[0 * n];
+        if (l2 >= 2) rp[-2] = bp[1 * n];
+        rp[0] = bp[2 * n];
+      }
+      lds_sync();
+    } else if constexpr (n >= 8) {
       // entry (ln, ln - 4) (positive immediate offsets) and the saved originals, saved by setup_qp
       double* rowp = P + ln * (kPS + 1) - 4;
       const double* bo = band + ln;
@@ -618,7 +675,25 @@ __device__ __forceinline__ bool setup_qp(const mpcqp_params& p, int b, const dou
   // symmetric Pbar = the lower triangle (row i >= column lane, computed by column `lane`)
   bool finite = isfinite(qv) && isfinite(cscale);
   lds_sync();  // setup's LDS data is dead: Pbar overwrites it
-  {
+  if constexpr (kPackedP<N>) {
+    double* Pb = lds.solve.P;
+    if (act) {
+#pragma unroll
+      for (int i = 0; i < n; ++i)
+        if (i >= lane) {  // entry (i, lane)
+          Pb[(i * (i + 1)) / 2 + lane] = Pc[i];
+          finite = finite && isfinite(Pc[i]);
+        }
+    }
+    for (int e = (n * (n + 1)) / 2 + lane; e < kWave * (kWave + 1) / 2; e += kWave) Pb[e] = 0.0;  // rows n..63
+    lds_sync();
+    if (act) {  // form()'s band addresses: save what they hold
+      const double* rowp = Pb + (lane * (lane + 1)) / 2 + lane;
+      lds.solve.band[0][lane] = lane >= 4 ? rowp[-4] : 0.0;
+      lds.solve.band[1][lane] = lane >= 2 ? rowp[-2] : 0.0;
+      lds.solve.band[2][lane] = rowp[0];
+    }
+  } else {
     constexpr int kPS = SolveSmem<N>::kPS;
     double* Pb = lds.solve.P;
     if (act) {
@@ -677,7 +752,8 @@ __device__ __forceinline__ bool setup_qp(const mpcqp_params& p, int b, const dou
   __syncthreads();
   if (dbg) {
     if (act)
-      for (int i = 0; i < n; ++i) dbg[i * n + lane] = lds.solve.P[i * SolveSmem<N>::kPS + lane];
+      for (int i = 0; i < n; ++i)
+        dbg[i * n + lane] = kPackedP<N> ? lds.solve.P[tri_idx(i, lane)] : lds.solve.P[i * SolveSmem<N>::kPS + lane];
     double* lf = dbg + state_lane_off(N);
     lf[kFq * kWave + lane] = qv;
     lf[kFD * kWave + lane] = D;
@@ -1220,11 +1296,11 @@ __device__ __forceinline__ void finish_qp(const mpcqp_params& p, int b, const do
 // registers for a third wave (168, fits the ~13 KB of LDS at N = 20) measured no faster at
 // B = 4096: the four QPs per SIMD then run in 1.33 rounds instead of 2, but each wave shares
 // its SIMD's FP64 issue with two others.
-// From N = 29 on the KKT inverse (2N doubles per lane) leaves 2 waves per SIMD no registers for
-// the rest of the working set, and Pbar (32 N^2 bytes of LDS) already limits a CU to 5
-// workgroups: the kernel takes the register file of 1 wave per SIMD instead of spilling.
+// From N = 29 on the KKT inverse (2N doubles per lane) fills the 256 registers of 2 waves per SIMD
+// (a handful of cold values spill, <= 64 bytes of scratch); Pbar packed (N >= 24) keeps the LDS at
+// eight workgroups per CU.  (Before: 1 wave per SIMD from N = 29, the LDS capping a CU at 5.)
 template <int N>
-constexpr int kSolveWavesPerEU = N >= 29 ? 1 : 2;
+constexpr int kSolveWavesPerEU = 2;
 
 template <int N>
 __global__ __launch_bounds__(kWave, kSolveWavesPerEU<N>) void k_solve(mpcqp_params p, int B, const uint8_t* __restrict__ mask,

@@ -268,11 +268,13 @@ def test_solver_kernel_resources():
     res = {int(k): v for k, v in json.loads(path.read_text()).items()}
     assert sorted(res) == list(range(1, 32))
     for N, r in res.items():
-        # N >= 29: Pbar's LDS already caps a CU at 5 workgroups; the kernel takes one wave's
-        # register file per SIMD (a few AGPRs as spill space) instead of scratch memory
-        assert r["Occupancy"] >= (2 if N <= 28 else 1), (N, r)
-        assert r["AGPRs"] == 0 or N >= 29, (N, r)
-        assert r["ScratchSize"] == 0, (N, r)
+        # every horizon at 2 waves per SIMD and 8 workgroups per CU (N >= 24: Pbar packed, <= 18 KB
+        # of LDS); N >= 29 fills
+        # the 256 registers and spills a handful of values outside the inverse (<= 64 bytes)
+        assert r["Occupancy"] >= 2, (N, r)
+        assert r["AGPRs"] == 0, (N, r)
+        assert r["ScratchSize"] <= (64 if N >= 29 else 0), (N, r)
+        assert r["LDS"] <= 160 * 1024 // 8, (N, r)  # 8 workgroups = 2 waves on each of 4 SIMDs
 
 
 def test_three_argument_step_resolves_parameters(golden, monkeypatch):
