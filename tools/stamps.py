@@ -45,8 +45,9 @@ def main() -> None:
     ap.add_argument("--worst", type=int, default=-1)
     ap.add_argument("--by", type=int, default=0, help="iteration counter ranking --worst (0 ADMM, 1 polish)")
     ap.add_argument("--batch", type=int, default=0)
+    ap.add_argument("--horizon", type=int, default=0, help="the config's generator at another horizon")
     a = ap.parse_args()
-    b = getattr(scenarios, a.config)()
+    b = getattr(scenarios, a.config)(**({"horizon": a.horizon} if a.horizon else {}))
     x0, ref, up = b.x0, b.ref, b.u_prev
     B = a.batch or b.size
     ctrl = BatchedMPCController(MPCConfig(horizon=b.horizon).to_parameters(0.8), max(B, b.size), device="cuda:0")
