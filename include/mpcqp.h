@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define MPCQP_ABI_VERSION 5
+#define MPCQP_ABI_VERSION 6
 
 /* error codes (function return values) */
 #define MPCQP_OK 0
@@ -217,6 +217,17 @@ int mpcqp_fleet_step(mpcqp_ws* nominal, mpcqp_ws* relaxed, const mpcqp_fleet* f,
  * internal stream (ordered after / before `stream` by events) and replays it `steps` times. */
 int mpcqp_fleet_run(mpcqp_ws* nominal, mpcqp_ws* relaxed, const mpcqp_fleet* f, int steps, int use_graph,
                     void* stream);
+
+/* `steps` steps of every RUNNING vehicle in ONE kernel launch (ABI 6): each vehicle's wave loops
+ * over its steps with no kernel boundary and no host round trip -- the same operations as
+ * mpcqp_fleet_run, so every output buffer (state, u_prev, path_idx, phase, steps, trace, u_trace,
+ * X, and status / u0 of each vehicle's last step) equals mpcqp_fleet_run's bit for bit (the mask
+ * scratch keeps each vehicle's last-step masks).  The loop does not write debug state.  Vehicles leave
+ * the loop at the goal, on abort or out of steps, so one call with steps = max_steps runs every
+ * vehicle to its end.  Horizons N <= 31 in fast mode without debug_state run the fused kernel;
+ * other parameter blocks (mid / long horizons, reproducible or debug_state) are executed by
+ * mpcqp_fleet_run's graph path. */
+int mpcqp_fleet_loop(mpcqp_ws* nominal, mpcqp_ws* relaxed, const mpcqp_fleet* f, int steps, void* stream);
 
 /*
  * Batched build_reference: src/control/ref_builder.py:10-22 with

@@ -91,6 +91,17 @@ const mpcqp::launcher_t kLaunchers[MPCQP_WIDE_MIN_HORIZON] = {
     MPCQP_L(16), MPCQP_L(17), MPCQP_L(18), MPCQP_L(19), MPCQP_L(20), MPCQP_L(21), MPCQP_L(22), MPCQP_L(23),
     MPCQP_L(24), MPCQP_L(25), MPCQP_L(26), MPCQP_L(27), MPCQP_L(28), MPCQP_L(29), MPCQP_L(30), MPCQP_L(31)};
 #undef MPCQP_L
+#ifdef MPCQP_ONLY_N
+#define MPCQP_F(N) ((N) == MPCQP_ONLY_N ? &mpcqp::launch_fleet_loop<MPCQP_ONLY_N> : nullptr)
+#else
+#define MPCQP_F(N) &mpcqp::launch_fleet_loop<N>
+#endif
+const mpcqp::fleet_loop_t kFleetLoops[MPCQP_WIDE_MIN_HORIZON] = {
+    nullptr,     MPCQP_F(1),  MPCQP_F(2),  MPCQP_F(3),  MPCQP_F(4),  MPCQP_F(5),  MPCQP_F(6),  MPCQP_F(7),
+    MPCQP_F(8),  MPCQP_F(9),  MPCQP_F(10), MPCQP_F(11), MPCQP_F(12), MPCQP_F(13), MPCQP_F(14), MPCQP_F(15),
+    MPCQP_F(16), MPCQP_F(17), MPCQP_F(18), MPCQP_F(19), MPCQP_F(20), MPCQP_F(21), MPCQP_F(22), MPCQP_F(23),
+    MPCQP_F(24), MPCQP_F(25), MPCQP_F(26), MPCQP_F(27), MPCQP_F(28), MPCQP_F(29), MPCQP_F(30), MPCQP_F(31)};
+#undef MPCQP_F
 
 // per-QP doubles of the solver state buffer (debug state of the one-wave kernel, the workspace
 // of the long-horizon kernel)
@@ -147,6 +158,10 @@ launcher_t launcher(const mpcqp_params& p) {
   if (wide_solve(p)) return p.reproducible == 0 && horizon <= MPCQP_MID_MAX_HORIZON ? &launch_mid : &launch_solve_wide;
   return horizon < MPCQP_WIDE_MIN_HORIZON ? kLaunchers[horizon] : nullptr;
 }
+fleet_loop_t fleet_looper(const mpcqp_params& p) {
+  if (wide_solve(p) || p.debug_state || p.horizon < 1 || p.horizon >= MPCQP_WIDE_MIN_HORIZON) return nullptr;
+  return kFleetLoops[p.horizon];
+}
 }  // namespace mpcqp
 
 extern "C" {
@@ -176,12 +191,15 @@ int mpcqp_create(const mpcqp_params* p, int max_batch, int device, mpcqp_ws** ws
   w->model = nullptr;
   w->state = nullptr;
   w->in_x0 = w->in_ref = w->in_up = nullptr;
+  w->dparams = nullptr;
   const size_t mbytes = sizeof(double) * (size_t)model_stride(p->horizon) * (size_t)max_batch;
   const size_t sbytes = sizeof(double) * ws_state_stride(p->horizon, mpcqp::wide_solve(*p)) * (size_t)max_batch;
   e = hipMalloc(&w->model, mbytes);
   if (e == hipSuccess) e = hipMalloc(&w->state, sbytes);
+  if (e == hipSuccess) e = hipMalloc(&w->dparams, 2 * sizeof(mpcqp_params));
   if (e != hipSuccess) {
     if (w->model) (void)hipFree(w->model);
+    if (w->state) (void)hipFree(w->state);
     delete w;
     return fail(MPCQP_E_HIP, std::string("hipMalloc: ") + hipGetErrorString(e));
   }
@@ -210,6 +228,7 @@ void mpcqp_destroy(mpcqp_ws* ws) {
   (void)hipSetDevice(ws->device);
   (void)hipFree(ws->model);
   (void)hipFree(ws->state);
+  (void)hipFree(ws->dparams);
   delete ws;
 }
 

@@ -147,4 +147,27 @@ __device__ __forceinline__ void build_qp_long(const mpcqp_params& p, int lane, F
   if (lane < 6) mb[11 * N + 4 + lane] = lane < 4 ? x0l : upl;
 }
 
+// ---- the closed loop's per-step arithmetic, shared by k_fleet_advance (mpcqp_fleet.hip) and the
+// fused loop k_fleet_loop (mpcqp_solve.h): numpy's operation order, no contraction.
+// vehicle_model.py:11-21
+__device__ __forceinline__ void plant(const double x[4], double a, double delta, double dt, double L, double out[4]) {
+#pragma clang fp contract(off)
+  out[0] = x[0] + dt * x[3] * cos(x[2]);
+  out[1] = x[1] + dt * x[3] * sin(x[2]);
+  out[2] = x[2] + dt * (x[3] / L) * tan(delta);
+  out[3] = x[3] + dt * a;
+}
+// path_idx advance test (control_stage.py:141-145): farther than 5 px from ref row r
+__device__ __forceinline__ bool fleet_off_row(double x, double y, const double* r) {
+#pragma clang fp contract(off)
+  const double dx = x - r[0];
+  const double dy = y - r[1];
+  return dx * dx + dy * dy > 25.0;
+}
+// goal test (control_stage.py:147-150)
+__device__ __forceinline__ bool fleet_at_goal(double x, double y, double gx, double gy) {
+#pragma clang fp contract(off)
+  return hypot(x - gx, y - gy) < 8.0;
+}
+
 }  // namespace

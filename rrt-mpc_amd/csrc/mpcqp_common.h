@@ -281,6 +281,13 @@ typedef void (*launcher_t)(hipStream_t, const Launch&);
 // mpcqp_part.hip objects (parallel build) or in mpcqp.hip itself (MPCQP_ONLY_N dev builds).
 template <int N>
 void launch_solve(hipStream_t s, const Launch& L);
+// the fused closed loop of a fleet (k_fleet_loop<N>, mpcqp_solve.h; N <= 31, fast mode): `steps`
+// loop steps of every RUNNING vehicle in one launch
+template <int N>
+void launch_fleet_loop(hipStream_t s, const mpcqp_params* P, const mpcqp_fleet& f, int steps);
+typedef void (*fleet_loop_t)(hipStream_t, const mpcqp_params*, const mpcqp_fleet&, int);
+// nullptr when the parameter block does not run the one-wave kernel; defined in mpcqp.hip
+fleet_loop_t fleet_looper(const mpcqp_params& p);
 // the long-horizon solve (N >= MPCQP_WIDE_MIN_HORIZON; mpcqp_wide.hip): one 256-thread workgroup
 // per QP, L.state = its workspace (wide_stride(N) doubles per QP)
 void launch_solve_wide(hipStream_t s, const Launch& L);
@@ -312,4 +319,8 @@ struct mpcqp_ws {
   const double* in_x0;
   const double* in_ref;
   const double* in_up;
+  // device copies of the parameter blocks of the last mpcqp_fleet_loop (nominal, relaxed): the fused
+  // loop selects its block per solve, which a kernel argument cannot be (the compiler copies a
+  // run-time-selected argument block to scratch); written by a kernel on the launch stream
+  mpcqp_params* dparams;
 };

@@ -64,15 +64,6 @@ __global__ __launch_bounds__(kWave) void k_fleet_build(mpcqp_params p, mpcqp_fle
   build_qp(p, lane, rx, ry, ryaw, rv, x0l, upl, model + (size_t)b * model_stride(N));
 }
 
-// vehicle_model.py:11-21, evaluated in numpy's operation order (no contraction)
-__device__ void plant(const double x[4], double a, double delta, double dt, double L, double out[4]) {
-#pragma clang fp contract(off)
-  out[0] = x[0] + dt * x[3] * cos(x[2]);
-  out[1] = x[1] + dt * x[3] * sin(x[2]);
-  out[2] = x[2] + dt * (x[3] / L) * tan(delta);
-  out[3] = x[3] + dt * a;
-}
-
 __global__ __launch_bounds__(kWave) void k_fleet_advance(double dt, double L, mpcqp_fleet f) {
 #pragma clang fp contract(off)
   const int b = blockIdx.x * kWave + threadIdx.x;
@@ -112,18 +103,24 @@ __global__ __launch_bounds__(kWave) void k_fleet_advance(double dt, double L, mp
   f.steps[b] = k + 1;
   const int len = f.ref_len[b];
   int pi = f.path_idx[b];
-  if (pi < len - 2) {
-    const double* r = f.ref_global + ((size_t)b * f.ref_stride + pi) * 4;
-    const double dx = xn[0] - r[0];
-    const double dy = xn[1] - r[1];
-    if (dx * dx + dy * dy > 25.0) f.path_idx[b] = pi + 1;
-  }
+  if (pi < len - 2 && fleet_off_row(xn[0], xn[1], f.ref_global + ((size_t)b * f.ref_stride + pi) * 4))
+    f.path_idx[b] = pi + 1;
   int ph = MPCQP_FLEET_RUNNING;
-  if (hypot(xn[0] - f.goal[(size_t)b * 2], xn[1] - f.goal[(size_t)b * 2 + 1]) < 8.0)
+  if (fleet_at_goal(xn[0], xn[1], f.goal[(size_t)b * 2], f.goal[(size_t)b * 2 + 1]))
     ph = MPCQP_FLEET_GOAL;
   else if (k + 1 >= f.max_steps)
     ph = MPCQP_FLEET_OUT_OF_STEPS;
   f.phase[b] = ph;
+}
+
+// the parameter blocks of one mpcqp_fleet_loop call, stream-ordered before the loop kernel
+__global__ __launch_bounds__(kWave) void k_store_params(mpcqp_params pn, mpcqp_params pr, mpcqp_params* __restrict__ P) {
+  static_assert(sizeof(mpcqp_params) % 4 == 0, "params copied by words");
+  constexpr int W = (int)(sizeof(mpcqp_params) / 4);
+  for (int w = threadIdx.x; w < W; w += kWave) {
+    reinterpret_cast<uint32_t*>(P)[w] = reinterpret_cast<const uint32_t*>(&pn)[w];
+    reinterpret_cast<uint32_t*>(P + 1)[w] = reinterpret_cast<const uint32_t*>(&pr)[w];
+  }
 }
 
 int check_fleet(const mpcqp_ws* nom, const mpcqp_ws* rel, const mpcqp_fleet* f) {
@@ -215,6 +212,26 @@ int mpcqp_fleet_step(mpcqp_ws* nominal, mpcqp_ws* relaxed, const mpcqp_fleet* f,
   if (rc) return rc;
   if (f->vehicles == 0) return MPCQP_OK;
   return enqueue_step(nominal, relaxed, f, static_cast<hipStream_t>(stream));
+}
+
+int mpcqp_fleet_loop(mpcqp_ws* nominal, mpcqp_ws* relaxed, const mpcqp_fleet* f, int steps, void* stream) {
+  int rc = check_fleet(nominal, relaxed, f);
+  if (rc) return rc;
+  if (steps < 0) return fail(MPCQP_E_ARG, "steps must be >= 0");
+  if (f->vehicles == 0 || steps == 0) return MPCQP_OK;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const mpcqp::fleet_loop_t loop = mpcqp::fleet_looper(nominal->p);
+  if (!loop || mpcqp::fleet_looper(relaxed->p) != loop)  // mid / long horizons, reproducible or debug mode
+    return run_graph(nominal, relaxed, f, steps, s);
+  nominal->built_B = -1;  // as mpcqp_fleet_step: a later mpcqp_solve needs its own build
+  relaxed->built_B = -1;
+  nominal->in_x0 = nominal->in_ref = nominal->in_up = nullptr;
+  relaxed->in_x0 = relaxed->in_ref = relaxed->in_up = nullptr;
+  hipLaunchKernelGGL(k_store_params, dim3(1), dim3(kWave), 0, s, nominal->p, relaxed->p, nominal->dparams);
+  loop(s, nominal->dparams, *f, steps);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return fail(MPCQP_E_HIP, std::string("k_fleet_loop launch: ") + hipGetErrorString(e));
+  return MPCQP_OK;
 }
 
 int mpcqp_fleet_run(mpcqp_ws* nominal, mpcqp_ws* relaxed, const mpcqp_fleet* f, int steps, int use_graph,

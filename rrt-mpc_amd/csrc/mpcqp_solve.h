@@ -381,6 +381,42 @@ struct Ctx {
   }
 };
 
+// ------------------------------------------------------------------ a QP's raw inputs
+// Where the fused K1 (setup_qp) and the outputs (finish_qp) read a QP's window, x0 and u_prev:
+// BatchWin = the caller's batch buffers (mpcqp_build / mpcqp_solve: the pointer arguments of
+// setup_qp / finish_qp, in_ref == nullptr when K1 ran as its own kernel), FleetWin = one vehicle of
+// the fused closed loop.
+struct BatchWin {
+  static constexpr bool kFleet = false;
+  __device__ __forceinline__ int lane() const { return threadIdx.x; }
+};
+// FleetWin: one vehicle of the fused closed loop (k_fleet_loop): window row k = the vehicle's
+// reference row min(path_idx + k, len - 1) (control_stage.py:101-105), speed x 0.6 in the relaxed
+// retry (:48-49); x0 / u_prev are the loop state.  The same gather as k_fleet_build.
+struct FleetWin {
+  static constexpr bool kFleet = true;
+  const double* __restrict__ rows;
+  int ln;  // the lane index, opaque per solve (k_fleet_loop)
+  int len, pidx;
+  bool relax;
+  double x[4], u[2];
+  template <int N>
+  __device__ __forceinline__ void row(int k, double& rx, double& ry, double& ryaw, double& rv) const {
+    const double* r = rows + (size_t)min(pidx + k, len - 1) * 4;
+    rx = r[0];
+    ry = r[1];
+    ryaw = r[2];
+    rv = relax ? r[3] * 0.6 : r[3];
+  }
+  __device__ __forceinline__ double x0l(int lane) const {
+    return lane == 0 ? x[0] : (lane == 1 ? x[1] : (lane == 2 ? x[2] : (lane == 3 ? x[3] : 0.0)));
+  }
+  __device__ __forceinline__ double upl(int lane) const { return lane == 4 ? u[0] : (lane == 5 ? u[1] : 0.0); }
+  __device__ __forceinline__ int lane() const { return ln; }
+  __device__ __forceinline__ double x0v(int i) const { return x[i]; }
+  __device__ __forceinline__ double upv(int i) const { return u[i]; }
+};
+
 // ------------------------------------------------------------------ K2 phase 1: setup
 // Condensing (states and slacks eliminated) + OSQP Ruiz/cost scaling.  Leaves the scaled
 // problem on chip for the later phases: Pbar (symmetric, row-major) in the solve LDS, the
@@ -392,16 +428,16 @@ struct Ctx {
 //   slot 1: input row        a_{p/2} or delta_{p/2}                    (:83-86)
 //   slot 2: rate row         U_p - U_{p-2} (u_prev at k = 0)           (:89-106)
 // the constant parts (v_0 = x0[3], u_prev) moved into the bounds.
-template <int N>
+template <int N, class Win>
 __device__ __forceinline__ bool setup_qp(const mpcqp_params& p, int b, const double* __restrict__ model,
                                          const double* __restrict__ in_x0, const double* __restrict__ in_ref,
-                                         const double* __restrict__ in_up, Ctx<N>& C, SolveLds<N>& lds,
+                                         const double* __restrict__ in_up, const Win& win, Ctx<N>& C, SolveLds<N>& lds,
                                          double* __restrict__ scratch, double* __restrict__ dbg) {
   constexpr int n = 2 * N;
   SetupSmem<N>& sm = lds.setup;
   (void)scratch;
   constexpr int S = model_stride(N);
-  const int lane = threadIdx.x;
+  const int lane = win.lane();
   const bool act = lane < n;
   const bool even = act && ((lane & 1) == 0);
   const int cc = lane & 1;  // 0 = acceleration, 1 = steering
@@ -410,7 +446,11 @@ __device__ __forceinline__ bool setup_qp(const mpcqp_params& p, int b, const dou
   T2.begin();
   T.begin();
 
-  if (in_ref) {  // K1 fused: the window -> LTV model straight into LDS (mpcqp_build.h)
+  if constexpr (Win::kFleet) {  // the fleet loop: the vehicle's window -> LTV model into LDS
+    double rx = 0.0, ry = 0.0, ryaw = 0.0, rv = 0.0;
+    if (lane <= N) win.template row<N>(lane, rx, ry, ryaw, rv);
+    build_qp(p, lane, rx, ry, ryaw, rv, win.x0l(lane), win.upl(lane), lds.model_ptr());
+  } else if (in_ref) {  // K1 fused: the window -> LTV model straight into LDS (mpcqp_build.h)
     const double* rb = in_ref + (size_t)b * (N + 1) * 4;
     double rx = 0.0, ry = 0.0, ryaw = 0.0, rv = 0.0;
     if (lane <= N) {
@@ -1143,17 +1183,18 @@ __device__ __forceinline__ void admm_debug_state(double* __restrict__ dbg, bool 
 // ------------------------------------------------------------------ K2c: status + outputs
 // x: the returned iterate (the polish's last iterate when the final polish ran), x_admm: the
 // ADMM iterate (returned when that polish did not converge, as OSQP does).
-template <int N>
-__device__ __forceinline__ void finish_qp(const mpcqp_params& p, int b, const double* __restrict__ model,
-                                          const double* __restrict__ in_x0, const double* __restrict__ in_ref,
-                                          const double* __restrict__ in_up, const double* kept_model, Ctx<N>& C,
+template <int N, class Win>
+__device__ __forceinline__ int finish_qp(const mpcqp_params& p, int b, const double* __restrict__ model,
+                                         const double* __restrict__ in_x0, const double* __restrict__ in_ref,
+                                         const double* __restrict__ in_up, const Win& win, const double* kept_model,
+                                         Ctx<N>& C,
                                           double x, double x_admm, int admm_flag, bool do_polish, bool pol_ok,
                                           bool bad, int admm_it, int nfact, int pol_it, int n_ls,
                                           double* __restrict__ u0o, double* __restrict__ Xo, double* __restrict__ Uo,
                                           int32_t* __restrict__ statuso, int32_t* __restrict__ iterso,
-                                          uint8_t* __restrict__ activeo) {
+                                          uint8_t* __restrict__ activeo, double& Uout) {
   constexpr int n = 2 * N;
-  const int lane = threadIdx.x;
+  const int lane = win.lane();
   const bool act = C.act;
   const bool use_admm = p.method == MPCQP_METHOD_ADMM;
   const bool approx = admm_flag == kAdmmApprox;  // OSQP's solved_inaccurate at max_iter: not polished
@@ -1178,7 +1219,7 @@ __device__ __forceinline__ void finish_qp(const mpcqp_params& p, int b, const do
   // the model's lane values: re-derived from the inputs when K1 is fused (the LDS copy is gone)
   double m_al = 0.0, m_be = 0.0, m_ga = 0.0, m_et = 0.0, m_si = 0.0, m_c0 = 0.0, m_c1 = 0.0;
   double x00, x01, x02, x03, up0, up1;
-  if (kModelKept<N>) {  // the model block is still in LDS
+  if constexpr (kModelKept<N>) {  // the model block is still in LDS
     const double* mb = kept_model;
     if (lane < N) {
       m_al = mb[lane];
@@ -1195,6 +1236,23 @@ __device__ __forceinline__ void finish_qp(const mpcqp_params& p, int b, const do
     x03 = mb[11 * N + 7];
     up0 = mb[11 * N + 8];
     up1 = mb[11 * N + 9];
+  } else if constexpr (Win::kFleet) {
+    double rx = 0.0, ry = 0.0, ryaw = 0.0, rv = 0.0;
+    if (lane <= N) win.template row<N>(lane, rx, ry, ryaw, rv);
+    const LaneModel m = build_lane(p, lane, ryaw, rv);
+    m_al = m.al;
+    m_be = m.be;
+    m_ga = m.ga;
+    m_et = m.et;
+    m_si = m.si;
+    m_c0 = m.c0;
+    m_c1 = m.c1;
+    x00 = win.x0v(0);
+    x01 = win.x0v(1);
+    x02 = win.x0v(2);
+    x03 = win.x0v(3);
+    up0 = win.upv(0);
+    up1 = win.upv(1);
   } else if (in_ref) {
     const double* rb = in_ref + (size_t)b * (N + 1) * 4;
     const double ryaw = lane <= N ? rb[4 * lane + 2] : 0.0, rv = lane <= N ? rb[4 * lane + 3] : 0.0;
@@ -1260,6 +1318,7 @@ __device__ __forceinline__ void finish_qp(const mpcqp_params& p, int b, const do
     Xb[2 * (N + 1) + lane] = pk;
     Xb[3 * (N + 1) + lane] = vk;
   }
+  Uout = U;
   if (Uo && act) Uo[(size_t)b * n + cc * N + (lane >> 1)] = U;
   if (u0o && lane < 2) u0o[(size_t)b * 2 + lane] = U;
   const double Um2 = shr2(U);
@@ -1283,42 +1342,25 @@ __device__ __forceinline__ void finish_qp(const mpcqp_params& p, int b, const do
       iterso[4 * (size_t)b + 3] = n_ls;
     }
   }
+  return status;
 }
 
-// ------------------------------------------------------------------ K2: fused solve
-// One wave runs its QP through setup -> ADMM -> polish/outputs without kernel boundaries, so
-// the batch drains once (the slowest QP's whole chain) instead of once per phase.  The scaled
-// problem never leaves the CU: Pbar stays in LDS, the per-lane data and the KKT inverse in
-// registers (the state buffer is written only when debug_state is set).
-// Occupancy: ~225 VGPRs (the KKT inverse is 2n of them) give 2 waves per SIMD; the launch
-// bound's 2 keeps the compiler from trading that for AGPR spills (a branch-free condensing
-// variant did, and ran at 1 wave per SIMD, +35 % at B = 4096).  Capping the
-// registers for a third wave (168, fits the ~13 KB of LDS at N = 20) measured no faster at
-// B = 4096: the four QPs per SIMD then run in 1.33 rounds instead of 2, but each wave shares
-// its SIMD's FP64 issue with two others.
-// From N = 29 on the KKT inverse (2N doubles per lane) fills the 256 registers of 2 waves per SIMD
-// (a handful of cold values spill, <= 64 bytes of scratch); Pbar packed (N >= 24) keeps the LDS at
-// eight workgroups per CU.  (Before: 1 wave per SIMD from N = 29, the LDS capping a CU at 5.)
-template <int N>
-constexpr int kSolveWavesPerEU = 2;
-
-template <int N>
-__global__ __launch_bounds__(kWave, kSolveWavesPerEU<N>) void k_solve(mpcqp_params p, int B, const uint8_t* __restrict__ mask,
-                                                 const double* __restrict__ model, const double* __restrict__ in_x0,
-                                                 const double* __restrict__ in_ref, const double* __restrict__ in_up,
-                                                 double* __restrict__ state,
-                                                 double* __restrict__ u0o, double* __restrict__ Xo,
-                                                 double* __restrict__ Uo, int32_t* __restrict__ statuso,
-                                                 int32_t* __restrict__ iterso, uint8_t* __restrict__ activeo) {
-  __shared__ SolveLds<N> sm;
-  const int b = blockIdx.x;
-  if (b >= B || (mask && !mask[b])) return;
-  double* dbg = p.debug_state ? state + (size_t)b * state_stride(N) : nullptr;
+// One QP through setup -> ADMM (+ early polish attempts) -> final polish -> outputs on the calling
+// wave, for the fused fleet loop (k_fleet_loop; no debug state): returns the status, Ulane = the
+// lane's U entry (lane 0/1: u0).  k_solve runs the same driver inline (below).
+template <int N, class Win>
+__device__ __forceinline__ int solve_one(const mpcqp_params& p, int b, const double* __restrict__ model,
+                                         const double* __restrict__ in_x0, const double* __restrict__ in_ref,
+                                         const double* __restrict__ in_up, const Win& win, SolveLds<N>& sm,
+                                         double* __restrict__ u0o, double* __restrict__ Xo, double* __restrict__ Uo,
+                                         int32_t* __restrict__ statuso, int32_t* __restrict__ iterso,
+                                         uint8_t* __restrict__ activeo, double& Ulane) {
+  double* const dbg = nullptr;
   const uint64_t t_start = __builtin_amdgcn_s_memtime();
   Stamps TK;
   TK.begin();
   Ctx<N> C;
-  bool bad = setup_qp<N>(p, b, model, in_x0, in_ref, in_up, C, sm, state + (size_t)b * state_stride(N), dbg);
+  bool bad = setup_qp<N>(p, b, model, in_x0, in_ref, in_up, win, C, sm, nullptr, dbg);
   const bool use_admm = p.method == MPCQP_METHOD_ADMM;
   AdmmState S;
   S.x = 0.0;
@@ -1386,8 +1428,8 @@ __global__ __launch_bounds__(kWave, kSolveWavesPerEU<N>) void k_solve(mpcqp_para
     if (S.rho_change) S.rho = S.rho_next;
     S.rho_change = false;
   }
-  finish_qp<N>(p, b, model, in_x0, in_ref, in_up, sm.model, C, x, x_admm, flag, do_polish, pol_ok, bad, S.it, S.nfact,
-               pol_it, n_ls, u0o, Xo, Uo, statuso, iterso, activeo);
+  const int status = finish_qp<N>(p, b, model, in_x0, in_ref, in_up, win, sm.model, C, x, x_admm, flag, do_polish, pol_ok, bad, S.it,
+                                  S.nfact, pol_it, n_ls, u0o, Xo, Uo, statuso, iterso, activeo, Ulane);
   TK.end(0);
   TK.flush(22);  // g_stamps[22]: the whole QP
   if (dbg && threadIdx.x == 0) {  // this wave's cycles, start to finish, and its work (tools/qp_cycles.py)
@@ -1395,6 +1437,222 @@ __global__ __launch_bounds__(kWave, kSolveWavesPerEU<N>) void k_solve(mpcqp_para
     dbg[state_scal_off(N) + 5] = (double)C.n_full;  // polish factorizations from scratch
     dbg[state_scal_off(N) + 6] = (double)C.n_r1;    // polish rank-1 updates
     dbg[state_scal_off(N) + 7] = (double)t_start;
+  }
+  return status;
+}
+
+// ------------------------------------------------------------------ K2: fused solve
+// One wave runs its QP through setup -> ADMM -> polish/outputs without kernel boundaries, so
+// the batch drains once (the slowest QP's whole chain) instead of once per phase.  The scaled
+// problem never leaves the CU: Pbar stays in LDS, the per-lane data and the KKT inverse in
+// registers (the state buffer is written only when debug_state is set).
+// Occupancy: ~225 VGPRs (the KKT inverse is 2n of them) give 2 waves per SIMD; the launch
+// bound's 2 keeps the compiler from trading that for AGPR spills (a branch-free condensing
+// variant did, and ran at 1 wave per SIMD, +35 % at B = 4096).  Capping the
+// registers for a third wave (168, fits the ~13 KB of LDS at N = 20) measured no faster at
+// B = 4096: the four QPs per SIMD then run in 1.33 rounds instead of 2, but each wave shares
+// its SIMD's FP64 issue with two others.
+// From N = 29 on the KKT inverse (2N doubles per lane) fills the 256 registers of 2 waves per SIMD
+// (a handful of cold values spill, <= 64 bytes of scratch); Pbar packed (N >= 24) keeps the LDS at
+// eight workgroups per CU.  (Before: 1 wave per SIMD from N = 29, the LDS capping a CU at 5.)
+template <int N>
+constexpr int kSolveWavesPerEU = 2;
+
+template <int N>
+__global__ __launch_bounds__(kWave, kSolveWavesPerEU<N>) void k_solve(mpcqp_params p, int B, const uint8_t* __restrict__ mask,
+                                                 const double* __restrict__ model, const double* __restrict__ in_x0,
+                                                 const double* __restrict__ in_ref, const double* __restrict__ in_up,
+                                                 double* __restrict__ state,
+                                                 double* __restrict__ u0o, double* __restrict__ Xo,
+                                                 double* __restrict__ Uo, int32_t* __restrict__ statuso,
+                                                 int32_t* __restrict__ iterso, uint8_t* __restrict__ activeo) {
+  __shared__ SolveLds<N> sm;
+  const int b = blockIdx.x;
+  if (b >= B || (mask && !mask[b])) return;
+  // solve_one's driver, kept inline here with the debug state: the headline kernel's code
+  // generation stays independent of the fleet loop's instantiation
+  double* dbg = p.debug_state ? state + (size_t)b * state_stride(N) : nullptr;
+  const uint64_t t_start = __builtin_amdgcn_s_memtime();
+  Stamps TK;
+  TK.begin();
+  Ctx<N> C;
+  bool bad = setup_qp<N>(p, b, model, in_x0, in_ref, in_up, BatchWin{}, C, sm, state + (size_t)b * state_stride(N), dbg);
+  const bool use_admm = p.method == MPCQP_METHOD_ADMM;
+  AdmmState S;
+  S.x = 0.0;
+#pragma unroll
+  for (int r = 0; r < 3; ++r) S.z[r] = S.y[r] = 0.0;
+  S.rho = S.rho_next = p.rho;
+  S.it = 0;
+  S.nfact = 0;
+  S.need_fact = true;
+  S.rho_change = false;
+  int flag = bad ? kAdmmBad : kAdmmMaxIter, pol_it = 0, n_ls = 0;
+  double x = 0.0, x_admm = 0.0;
+  bool do_polish = false, pol_ok = false;
+  if (use_admm && bad) admm_debug_state<N>(dbg, C.act, 0.0, flag, 0, 0);
+  // ADMM with its early polish attempts, then the final polish: ONE polish call site
+  while (!bad) {
+    // kind 1: early attempt (ADMM resumes if it fails), 2: final polish (OSQP polishes only a
+    // solved ADMM run; method newton is the polish alone, from x = 0)
+    int kind = 0;
+    double zg[3];
+    if (use_admm) {
+      const int ev = admm_run<N>(p, C, S);
+      if (ev == kAdmmAttempt) {
+        kind = 1;
+      } else {
+        flag = ev;
+        x = x_admm = C.act ? S.x : 0.0;
+        admm_debug_state<N>(dbg, C.act, x, flag, S.it, S.nfact);
+        do_polish = p.polish != 0 && flag == kAdmmConverged;
+        kind = do_polish ? 2 : 0;
+        bad = flag == kAdmmBad;
+      }
+#pragma unroll
+      for (int r = 0; r < 3; ++r) zg[r] = S.z[r];  // first active-set guess: the ADMM z iterate
+    } else {
+      do_polish = true;
+      kind = 2;
+      C.Cmul(x, zg);
+    }
+    if (kind == 0) break;
+    double xp = kind == 1 ? S.x : x;
+    Stamps T2;
+    T2.begin();
+    const int r_ = polish_qp<N>(C, xp, zg, kind == 1 ? p.polish_attempt_max_iter : p.polish_max_iter, pol_it,
+                                S.nfact, n_ls);
+    T2.end(0);
+    T2.flush(12);  // g_stamps[12]: polish
+    if (kind == 2) {  // final polish: its iterate is returned when it converged
+      x = xp;
+      bad = r_ < 0;
+      pol_ok = r_ > 0;
+      break;
+    }
+    if (r_ != 0) {  // the attempt reached the exact optimum (ADMM flag 2) or failed numerically
+      flag = r_ > 0 ? 2 : kAdmmBad;
+      bad = r_ < 0;
+      pol_ok = r_ > 0;
+      x = x_admm = C.act ? (pol_ok ? xp : S.x) : 0.0;
+      admm_debug_state<N>(dbg, C.act, x, flag, S.it, S.nfact);
+      break;
+    }
+    // a failed attempt resumes ADMM: refactor (the attempt used the inverse's registers) with
+    // the rho of that check's adaptive update
+    S.need_fact = true;
+    if (S.rho_change) S.rho = S.rho_next;
+    S.rho_change = false;
+  }
+  double U;
+  finish_qp<N>(p, b, model, in_x0, in_ref, in_up, BatchWin{}, sm.model, C, x, x_admm, flag, do_polish, pol_ok, bad, S.it,
+               S.nfact, pol_it, n_ls, u0o, Xo, Uo, statuso, iterso, activeo, U);
+  TK.end(0);
+  TK.flush(22);  // g_stamps[22]: the whole QP
+  if (dbg && threadIdx.x == 0) {  // this wave's cycles, start to finish, and its work (tools/qp_cycles.py)
+    dbg[state_scal_off(N) + 4] = (double)(__builtin_amdgcn_s_memtime() - t_start);
+    dbg[state_scal_off(N) + 5] = (double)C.n_full;  // polish factorizations from scratch
+    dbg[state_scal_off(N) + 6] = (double)C.n_r1;    // polish rank-1 updates
+    dbg[state_scal_off(N) + 7] = (double)t_start;
+  }
+}
+
+// ------------------------------------------------------------------ fused closed loop
+// Every vehicle of a fleet runs `steps` iterations of the loop body of TrajectoryTracker.track
+// (control_stage.py:100-150) on its own wave, with no kernel boundary between steps: the window
+// gather fused into K1 (:101-105), the nominal solve and the relaxed retry (:33-56), abort
+// (:108-110), the plant (:127), u_prev (:129), the path_idx advance (:141-145) and the goal test
+// (:147-150) -- the operations of k_fleet_build / k_solve / k_fleet_advance (mpcqp_fleet.hip) in the
+// same order, so the traces equal mpcqp_fleet_run's bit for bit.  The loop state (x, u_prev) stays
+// in LDS across steps (no registers held through the solve); it is written back at the end.
+template <int N>
+__global__ __launch_bounds__(kWave, kSolveWavesPerEU<N>) void k_fleet_loop(const mpcqp_params* __restrict__ P,
+                                                                         mpcqp_fleet f, int steps) {
+  __shared__ SolveLds<N> sm;
+  __shared__ double ls[6];  // loop state: x[4], u_prev[2]
+  const int b = blockIdx.x;
+  const int lane = threadIdx.x;
+  const int V = f.vehicles;
+  if (b >= V) return;
+  int phase = f.phase[b];
+  if (phase != MPCQP_FLEET_RUNNING) return;
+  const int len = f.ref_len[b];
+  int pidx = f.path_idx[b];
+  int k = f.steps[b];
+  const double* rows = f.ref_global + (size_t)b * f.ref_stride * 4;
+  if (lane < 4) ls[lane] = f.state[(size_t)b * 4 + lane];
+  else if (lane < 6) ls[lane] = f.u_prev[(size_t)b * 2 + lane - 4];
+  __syncthreads();
+  for (int s = 0; s < steps; ++s) {
+    // k_fleet_build's validation of the loop state, before any indexed access
+    const bool bad_ref = len < 1 || len > f.ref_stride || pidx < 0;
+    const bool full = k < 0 || k >= f.max_steps;
+    if (bad_ref || full) {
+      phase = bad_ref ? MPCQP_FLEET_ABORTED : MPCQP_FLEET_OUT_OF_STEPS;
+      if (lane == 0) f.mask[b] = 0;
+      break;
+    }
+    int which = -1;
+    double U = 0.0;
+#pragma nounroll
+    for (int relax = 0; relax < 2; ++relax) {
+      // the lane index and the parameter block opaque per solve: otherwise LICM hoists every
+      // lane- and parameter-derived value of the solver out of the step loop and holds it through
+      // the whole run (hundreds of registers of spills)
+      int ln = lane;
+      asm volatile("" : "+v"(ln));
+      const mpcqp_params& p = P[relax];  // P = {nominal, relaxed} in global memory (ws->dparams)
+      FleetWin win{rows, ln, len, pidx, relax != 0, {ls[0], ls[1], ls[2], ls[3]}, {ls[4], ls[5]}};
+      double Ul;
+      const int st = solve_one<N>(p, b, nullptr, nullptr, nullptr, nullptr, win, sm, f.u0 + (size_t)relax * V * 2, f.X, nullptr,
+                                  f.status + (size_t)relax * V, nullptr, nullptr, Ul);
+      __syncthreads();  // the next solve (or step) reuses the LDS
+      if (lane == 0) f.mask[(size_t)relax * V + b] = 1;
+      if (st == MPCQP_SOLVED || st == MPCQP_SOLVED_INACCURATE) {
+        which = relax;
+        U = Ul;
+        break;
+      }
+    }
+    if (which == 0 && lane == 0) f.mask[(size_t)V + b] = 0;
+    if (which < 0) {
+      phase = MPCQP_FLEET_ABORTED;  // control_stage.py:108-110
+      break;
+    }
+    // k_fleet_advance (every lane computes the same values)
+    const double a = readlane(U, 0), delta = readlane(U, 1);
+    double x[4] = {ls[0], ls[1], ls[2], ls[3]}, xn[4];
+    plant(x, a, delta, P[0].dt, P[0].wheelbase_px, xn);
+    if (lane == 0) {
+      if (f.trace)
+        for (int i = 0; i < 4; ++i) f.trace[((size_t)b * f.max_steps + k) * 4 + i] = xn[i];
+      if (f.u_trace) {
+        f.u_trace[((size_t)b * f.max_steps + k) * 2 + 0] = a;
+        f.u_trace[((size_t)b * f.max_steps + k) * 2 + 1] = delta;
+      }
+    }
+    __syncthreads();
+    if (lane < 4) ls[lane] = xn[lane];
+    else if (lane == 4) ls[4] = a;
+    else if (lane == 5) ls[5] = delta;
+    __syncthreads();
+    k = k + 1;
+    if (pidx < len - 2 && fleet_off_row(xn[0], xn[1], rows + (size_t)pidx * 4)) pidx = pidx + 1;
+    if (fleet_at_goal(xn[0], xn[1], f.goal[(size_t)b * 2], f.goal[(size_t)b * 2 + 1])) {
+      phase = MPCQP_FLEET_GOAL;
+      break;
+    }
+    if (k >= f.max_steps) {
+      phase = MPCQP_FLEET_OUT_OF_STEPS;
+      break;
+    }
+  }
+  if (lane < 4) f.state[(size_t)b * 4 + lane] = ls[lane];
+  else if (lane < 6) f.u_prev[(size_t)b * 2 + lane - 4] = ls[lane];
+  if (lane == 0) {
+    f.path_idx[b] = pidx;
+    f.steps[b] = k;
+    f.phase[b] = phase;
   }
 }
 
@@ -1406,6 +1664,10 @@ void launch_solve(hipStream_t s, const Launch& L) {
   hipLaunchKernelGGL(k_solve<N>, dim3(L.B), dim3(kWave), 0, s, *L.p, L.B, L.mask, L.model, L.x0, L.ref, L.u_prev,
                      L.state, L.u0, L.X, L.U,
                      L.st, L.it, L.ac);
+}
+template <int N>
+void launch_fleet_loop(hipStream_t s, const mpcqp_params* P, const mpcqp_fleet& f, int steps) {
+  hipLaunchKernelGGL(k_fleet_loop<N>, dim3(f.vehicles), dim3(kWave), 0, s, P, f, steps);
 }
 
 }  // namespace mpcqp

@@ -34,7 +34,7 @@ STATUS_NAMES = {
 
 # OSQP settings used by the reference (src/control/mpc_controller.py:121-131) plus the
 # OSQP defaults it relies on implicitly.
-ABI_VERSION = 5  # MPCQP_ABI_VERSION (include/mpcqp.h)
+ABI_VERSION = 6  # MPCQP_ABI_VERSION (include/mpcqp.h)
 
 DEFAULT_SOLVER_SETTINGS = dict(
     rho=0.1,
@@ -230,6 +230,8 @@ _SYMBOLS = {
                          ctypes.c_int),
     "mpcqp_fleet_run": ([ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(MpcqpFleet), ctypes.c_int, ctypes.c_int,
                          ctypes.c_void_p], ctypes.c_int),
+    "mpcqp_fleet_loop": ([ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(MpcqpFleet), ctypes.c_int,
+                          ctypes.c_void_p], ctypes.c_int),
     "mpcqp_build_reference": ([ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_double,
                                ctypes.c_int, ctypes.c_double, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
                                ctypes.c_void_p], ctypes.c_int),
@@ -270,12 +272,15 @@ def lib() -> ctypes.CDLL:
             "(hipcc --offload-arch=gfx950).  The MPC solver has no CPU fallback."
         )
     handle = ctypes.CDLL(str(LIB_PATH))
+    any_abi = bool(os.environ.get("MPCQP_ABI_ANY"))
     for name, (argtypes, restype) in _SYMBOLS.items():
+        if any_abi and not hasattr(handle, name):  # an older build lacks the newer entry points
+            continue
         fn = getattr(handle, name)
         fn.argtypes = argtypes
         fn.restype = restype
     # MPCQP_ABI_ANY: development A/B runs against an older kernel build (tools/diag)
-    if handle.mpcqp_version() != ABI_VERSION and not os.environ.get("MPCQP_ABI_ANY"):
+    if handle.mpcqp_version() != ABI_VERSION and not any_abi:
         raise LibraryError(f"libmpcqp ABI version {handle.mpcqp_version()} != {ABI_VERSION}")
     _lib = handle
     return handle

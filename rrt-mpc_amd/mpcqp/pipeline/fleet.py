@@ -6,6 +6,10 @@
 with the reference's relaxation retry (``:33-56``), the plant ``f_discrete`` (``:127``),
 the ``path_idx`` advance (``:141-145``) and the goal test (``:147-150``), all on the
 device.  The host only checks every ``check_every`` steps whether any vehicle still runs.
+``fused=True`` runs the whole loop in ONE launch instead (``mpcqp_fleet_loop``,
+``k_fleet_loop`` in ``csrc/mpcqp_solve.h``): each vehicle's wave loops over its own steps, with
+no kernel boundary per step, and leaves the loop at its goal -- the same operations, so the
+traces are bit-identical to the stepped path.
 
 Each vehicle follows exactly the reference's single-vehicle semantics, so vehicle ``v``
 reproduces ``TrajectoryTracker.track`` on its own plan (tests/test_gpu_fleet.py).
@@ -72,8 +76,8 @@ class FleetTracker:
     """
 
     def __init__(self, mpc, *, map_resolution: float, max_vehicles: int, max_ref_len: int,
-                 device=None, use_graph: bool = True, relaxed_settings: Optional[dict] = None,
-                 **settings) -> None:
+                 device=None, use_graph: bool = True, fused: bool = False,
+                 relaxed_settings: Optional[dict] = None, **settings) -> None:
         import torch
 
         from ..control.mpc_controller import BatchedMPCController
@@ -85,6 +89,7 @@ class FleetTracker:
         self.max_vehicles = int(max_vehicles)
         self.max_ref_len = int(max_ref_len)
         self.use_graph = bool(use_graph)
+        self.fused = bool(fused)
         self._nominal = BatchedMPCController(self.params, self.max_vehicles, device=device, **settings)
         # the retry's solver settings default to the nominal ones (control_stage.py:50-56 changes
         # only du_bounds and the reference speed)
@@ -198,6 +203,10 @@ class FleetTracker:
         if stream is None:
             stream = torch.cuda.current_stream(self.device)
         s = ctypes.c_void_p(stream.cuda_stream)
+        if self.fused:
+            _lib.check(self._L.mpcqp_fleet_loop(self._nominal._ws, self._relaxed._ws, ctypes.byref(self._fleet),
+                                                int(steps), s), "mpcqp_fleet_loop")
+            return
         _lib.check(self._L.mpcqp_fleet_run(self._nominal._ws, self._relaxed._ws, ctypes.byref(self._fleet),
                                            int(steps), int(self.use_graph), s), "mpcqp_fleet_run")
 
@@ -207,6 +216,10 @@ class FleetTracker:
     def run(self, sim_steps: Optional[int] = None, check_every: int = 16) -> FleetResult:
         """Step until every vehicle has left the RUNNING phase (or ``sim_steps`` steps)."""
         total = self.max_steps if sim_steps is None else min(int(sim_steps), self.max_steps)
+        if self.fused:  # one launch: every vehicle leaves the loop by itself
+            if self.vehicles:
+                self.step(total)
+            return self.result()
         done = 0
         while done < total and self.vehicles:
             k = min(check_every, total - done)

@@ -36,23 +36,24 @@ def _branches(golden):
     return [br["spline"][off[i]:off[i + 1]] for i in range(len(off) - 1)]
 
 
-def _tracker(N, V, M, sim_steps, map_resolution=0.8, use_graph=True):
+def _tracker(N, V, M, sim_steps, map_resolution=0.8, use_graph=True, fused=False):
     from mpcqp.config import MPCConfig
     from mpcqp.pipeline.fleet import FleetTracker
 
     mpc = MPCConfig(horizon=N, sim_steps=sim_steps)
     return FleetTracker(mpc, map_resolution=map_resolution, max_vehicles=V, max_ref_len=M, device="cuda:0",
-                        use_graph=use_graph)
+                        use_graph=use_graph, fused=fused)
 
 
+@pytest.mark.parametrize("fused", [False, True])
 @pytest.mark.parametrize("N,sim_steps", [(10, 100), (15, 300)])
-def test_fleet_reproduces_reference_closed_loop(cuda, golden, N, sim_steps):
+def test_fleet_reproduces_reference_closed_loop(cuda, golden, N, sim_steps, fused):
     from mpcqp import _lib
 
     g, path = _default_plan(golden)
     loop = golden("closed_loop.npz")
     V = 16
-    ft = _tracker(N, V, 64, sim_steps, float(g["map_resolution"]))
+    ft = _tracker(N, V, 64, sim_steps, float(g["map_resolution"]), fused=fused)
     ft.reset_from_plans([path] * V, np.tile(g["start"], (V, 1)), np.tile(g["goal"], (V, 1)))
     res = ft.run()
     ref_states = loop[f"N{N}_states"]
@@ -187,3 +188,82 @@ def test_fleet_large_batch_properties(cuda, golden):
             nxt = mo.f_discrete(x[k - 1], u[k], params.dt, params.wheelbase_px)
             np.testing.assert_allclose(x[k], nxt, rtol=0, atol=1e-9)
     ft.close()
+
+
+# every buffer the loop owns (the masks are scratch: the stepped path clears them for vehicles that
+# no longer run, the fused loop leaves each vehicle's last-step masks)
+_LOOP_BUFFERS = ("state", "u_prev", "path_idx", "phase", "steps", "trace", "u_trace", "X", "status", "u0")
+
+
+@pytest.mark.parametrize("N,V,steps,seed", [(10, 40, 60, 3), (20, 300, 45, 7), (24, 64, 30, 9), (30, 64, 30, 13)])
+def test_fused_loop_equals_stepped_loop_bitwise(cuda, golden, N, V, steps, seed):
+    """mpcqp_fleet_loop (one launch, k_fleet_loop) == mpcqp_fleet_run (graph-replayed steps), every
+    output buffer bit for bit: N = 10 / 20 keep the model block in LDS, N = 24 / 30 re-derive it
+    from the window for the outputs (packed Pbar), N = 30 at the register limit."""
+    g, paths, starts, goals = _varied_fleet(golden, V, seed=seed)
+    bufs = []
+    for fused in (False, True):
+        ft = _tracker(N, V, 128, steps, fused=fused)
+        ft.reset_from_plans(paths, starts, goals)
+        res = ft.run()
+        bufs.append({k: ft.buffers()[k].cpu().numpy().copy() for k in _LOOP_BUFFERS})
+        ft.close()
+    a, b = bufs
+    for k in _LOOP_BUFFERS:
+        np.testing.assert_array_equal(a[k], b[k], err_msg=k)
+    assert (res.phase != 0).all() or (res.steps == steps).all()
+
+
+def test_fused_loop_partial_runs_and_resume(cuda, golden):
+    """steps < needed: the fused loop stops every vehicle after that many steps and a second call
+    resumes from the device state -- the same as stepping."""
+    N, V = 15, 24
+    g, paths, starts, goals = _varied_fleet(golden, V, seed=17)
+    out = []
+    for fused in (False, True):
+        ft = _tracker(N, V, 128, 80, fused=fused)
+        ft.reset_from_plans(paths, starts, goals)
+        ft.step(7)
+        ft.step(11)
+        res = ft.run()
+        out.append((res, {k: ft.buffers()[k].cpu().numpy().copy() for k in _LOOP_BUFFERS}))
+        ft.close()
+    for k in _LOOP_BUFFERS:
+        np.testing.assert_array_equal(out[0][1][k], out[1][1][k], err_msg=k)
+
+
+def test_fused_loop_unsolvable_vehicle_aborts_alone(cuda, golden):
+    from mpcqp import _lib
+
+    N, steps, V = 10, 20, 6
+    g, path = _default_plan(golden)
+    ft = _tracker(N, V, 64, steps, float(g["map_resolution"]), fused=True)
+    ft.reset_from_plans([path] * V, np.tile(g["start"], (V, 1)), np.tile(g["goal"], (V, 1)))
+    ft.buffers()["state"][2, 0] = float("nan")
+    res = ft.run()
+    b = ft.buffers()
+    assert b["mask"][:, 2].cpu().tolist() == [1, 1]  # nominal solve, then the relaxed retry
+    assert (b["status"][:, 2].cpu().numpy() == _lib.NUMERICAL_ERROR).all()
+    assert res.phase[2] == _lib.FLEET_ABORTED and res.steps[2] == 0
+    others = [v for v in range(V) if v != 2]
+    assert (res.phase[others] == _lib.FLEET_OUT_OF_STEPS).all() and (res.steps[others] == steps).all()
+    loop = golden("closed_loop.npz")
+    for v in others:
+        np.testing.assert_allclose(res.states[v], loop["N10_states"][:steps], rtol=0, atol=ATOL)
+    ft.close()
+
+
+def test_fused_loop_falls_back_past_one_wave(cuda, golden):
+    """Horizons past the one-wave kernel (N = 40, mid kernel) run mpcqp_fleet_loop through the
+    stepped graph path: the same results as mpcqp_fleet_run."""
+    N, V, steps = 40, 8, 12
+    g, paths, starts, goals = _varied_fleet(golden, V, seed=23)
+    bufs = []
+    for fused in (False, True):
+        ft = _tracker(N, V, 160, steps, fused=fused)
+        ft.reset_from_plans(paths, starts, goals)
+        ft.run()
+        bufs.append({k: ft.buffers()[k].cpu().numpy().copy() for k in _LOOP_BUFFERS})
+        ft.close()
+    for k in _LOOP_BUFFERS:
+        np.testing.assert_array_equal(bufs[0][k], bufs[1][k], err_msg=k)

@@ -140,7 +140,8 @@ def test_relaxed_retry_succeeds_host(cuda):
     assert _rel(U, nom.Umat) > 1e-3
 
 
-def test_relaxed_retry_succeeds_fleet(cuda):
+@pytest.mark.parametrize("fused", [False, True])
+def test_relaxed_retry_succeeds_fleet(cuda, fused):
     """The same branch in the device fleet (k_fleet_build relax=1 + the relaxed workspace): one
     step of 8 vehicles whose nominal workspace cannot solve; applied input and next state equal
     the oracle's relaxed optimum and f_discrete."""
@@ -154,7 +155,7 @@ def test_relaxed_retry_succeeds_fleet(cuda):
     paths, starts, goals = scenarios.fleet5(8, seed=11)
     mpc = MPCConfig(horizon=N, sim_steps=3)
     ft = FleetTracker(mpc, map_resolution=0.8, max_vehicles=8, max_ref_len=160, device="cuda:0",
-                      use_graph=False, relaxed_settings={}, **FAIL_NOMINAL)
+                      use_graph=False, fused=fused, relaxed_settings={}, **FAIL_NOMINAL)
     refs = ft.reset_from_plans(paths, starts, goals)
     ft.step(1)
     res = ft.result()

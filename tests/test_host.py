@@ -35,7 +35,7 @@ def test_library_exports_every_header_symbol():
         assert hasattr(handle, name), f"{name} declared in include/mpcqp.h but not exported"
     assert set(decls) == set(_lib_mod.exported_symbols())
     L = _lib_mod.lib()
-    assert L.mpcqp_version() == _lib_mod.ABI_VERSION == 5
+    assert L.mpcqp_version() == _lib_mod.ABI_VERSION == 6
     assert L.mpcqp_num_rows(20) == 101
     assert L.mpcqp_model_stride(20) % 8 == 0
 
@@ -265,8 +265,17 @@ def test_solver_kernel_resources():
     path = ROOT / "build" / "kernel_resources.json"
     if not path.exists():
         pytest.skip("library not built in this tree (build() writes the resource record)")
-    res = {int(k): v for k, v in json.loads(path.read_text()).items()}
+    rec = json.loads(path.read_text())
+    res = {int(k): v for k, v in rec.items() if not k.startswith("loop:")}
+    loops = {int(k.split(":")[1]): v for k, v in rec.items() if k.startswith("loop:")}
     assert sorted(res) == list(range(1, 32))
+    assert sorted(loops) == list(range(1, 32))
+    for N, r in loops.items():
+        # the fused closed loop (k_fleet_loop<N>) runs the same solver at 2 waves per SIMD; values
+        # live across the steps (loop state, output pointers) spill at the step boundary only
+        assert r["Occupancy"] >= 2 and r["AGPRs"] == 0, (N, r)
+        assert r["ScratchSize"] <= 512, (N, r)
+        assert r["LDS"] <= 160 * 1024 // 8, (N, r)
     for N, r in res.items():
         # every horizon at 2 waves per SIMD and 8 workgroups per CU (N >= 24: Pbar packed, <= 18 KB
         # of LDS); N >= 29 fills

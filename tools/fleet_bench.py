@@ -1,11 +1,12 @@
 #!/usr/bin/env python3
 """Closed-loop fleet benchmark (BASELINE config 5 style): V vehicles on
 RRT*-branch plans, references built on the device, `sim_steps` closed-loop MPC steps each, every
-step on the GPU (mpcqp_fleet_run, hipGraph replay).  Reports vehicle-steps/s (one vehicle-step =
+step on the GPU (mpcqp_fleet_run, hipGraph replay per step; --fused: mpcqp_fleet_loop, the whole
+loop in one launch).  Reports vehicle-steps/s (one vehicle-step =
 window + nominal QP (+ relaxed retry) + plant + path_idx/goal update) and, for scale, the
 reference-style host loop (TrajectoryTracker.track, one B=1 solve per step) on one vehicle.
 
-    python tools/fleet_bench.py [--vehicles 100 1024 4096] [--steps 100] [--horizon 15]
+    python tools/fleet_bench.py [--vehicles 100 1024 4096] [--steps 100] [--horizon 15] [--fused]
 """
 from __future__ import annotations
 
@@ -28,6 +29,7 @@ def main() -> None:
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--horizon", type=int, default=15)
     ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--fused", action="store_true", help="mpcqp_fleet_loop: one launch for the whole loop")
     a = ap.parse_args()
     import torch
 
@@ -37,11 +39,12 @@ def main() -> None:
     from mpcqp.pipeline.fleet import FleetTracker
 
     dev = torch.device("cuda:0")
-    out = {"metric": "closed-loop vehicle-steps/s", "horizon": a.horizon, "sim_steps": a.steps, "runs": []}
+    out = {"metric": "closed-loop vehicle-steps/s", "horizon": a.horizon, "sim_steps": a.steps,
+           "mode": "fused loop (mpcqp_fleet_loop)" if a.fused else "graph-replayed steps (mpcqp_fleet_run)", "runs": []}
     for V in a.vehicles:
         paths, starts, goals = scenarios.fleet5(V)
         mpc = MPCConfig(horizon=a.horizon, sim_steps=a.steps)
-        ft = FleetTracker(mpc, map_resolution=0.8, max_vehicles=V, max_ref_len=160, device=dev)
+        ft = FleetTracker(mpc, map_resolution=0.8, max_vehicles=V, max_ref_len=160, device=dev, fused=a.fused)
         best = None
         for r in range(a.reps + 1):
             torch.cuda.synchronize()
