@@ -17,11 +17,6 @@
 #include "mpcqp_solve.h"  // development builds: one horizon, one translation unit
 #endif
 
-// development: the first horizon of the long-horizon kernel (A/B builds only; the product uses
-// MPCQP_WIDE_MIN_HORIZON)
-#ifndef MPCQP_WIDE_FROM
-#define MPCQP_WIDE_FROM MPCQP_WIDE_MIN_HORIZON
-#endif
 
 namespace {
 using mpcqp::Launch;
@@ -149,7 +144,7 @@ int fail(int code, const std::string& msg) {
   g_err = msg;
   return code;
 }
-bool wide_solve(const mpcqp_params& p) { return p.horizon >= MPCQP_WIDE_FROM || p.reproducible != 0; }
+bool wide_solve(const mpcqp_params& p) { return p.horizon >= MPCQP_WIDE_MIN_HORIZON || p.reproducible != 0; }
 launcher_t launcher(const mpcqp_params& p) {
   const int horizon = p.horizon;
   if (horizon < 1 || horizon > MPCQP_MAX_HORIZON) return nullptr;
@@ -273,7 +268,7 @@ const double* mpcqp_model_buffer(const mpcqp_ws* ws) { return ws ? ws->model : n
 
 const double* mpcqp_state_buffer(const mpcqp_ws* ws) { return ws ? ws->state : nullptr; }
 
-int mpcqp_state_stride(int horizon) { return (int)ws_state_stride(horizon, horizon >= MPCQP_WIDE_FROM); }
+int mpcqp_state_stride(int horizon) { return (int)ws_state_stride(horizon, horizon >= MPCQP_WIDE_MIN_HORIZON); }
 
 int mpcqp_ws_state_stride(const mpcqp_ws* ws) {
   if (!ws) return fail(MPCQP_E_ARG, "null ws");

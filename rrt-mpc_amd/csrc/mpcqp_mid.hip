@@ -47,9 +47,7 @@ struct MidStamps {
   __device__ __forceinline__ void flush() {}
 };
 #endif
-#ifndef MPCQP_MID_WAVES  // waves per SIMD the register allocation targets
-#define MPCQP_MID_WAVES 2
-#endif
+constexpr int kMidWaves = 2;  // waves per SIMD the register allocation targets
 
 // f(c, ld(c)) for c in [0, NT), the loads issued one group of G ahead of their uses and no further
 // (a scheduling barrier per group): the operand column never occupies more than 2 G registers next to
@@ -1141,7 +1139,7 @@ __device__ __forceinline__ void mid_finish(const mpcqp_params& p, int b, Mid<NT>
 
 // ------------------------------------------------------------------ the kernel
 template <int NT>
-__global__ __launch_bounds__(MidShape<NT>::kThreads, MPCQP_MID_WAVES) void k_solve_mid(
+__global__ __launch_bounds__(MidShape<NT>::kThreads, kMidWaves) void k_solve_mid(
     mpcqp_params p, int B, const uint8_t* __restrict__ mask, const double* __restrict__ model,
     double* __restrict__ work, double* __restrict__ u0o, double* __restrict__ Xo, double* __restrict__ Uo,
     int32_t* __restrict__ statuso, int32_t* __restrict__ iterso, uint8_t* __restrict__ activeo) {

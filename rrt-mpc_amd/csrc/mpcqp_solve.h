@@ -13,11 +13,8 @@ using mpcqp::Launch;
 // for 64 rows, rows n..63 zero: 16.6 KB instead of 32 N^2 bytes, so eight workgroups fit a CU's LDS
 // (the full matrix allowed 7 at N = 24, 5 from N = 28 on) and the kernel runs 2 waves per SIMD (Pbar is read only by form() and Pmul: a factorization or a
 // residual check, not per ADMM iteration).
-#ifndef MPCQP_PACKED_FROM
-#define MPCQP_PACKED_FROM 24
-#endif
 template <int N>
-constexpr bool kPackedP = N >= MPCQP_PACKED_FROM;
+constexpr bool kPackedP = N >= 24;
 
 template <int N, bool Packed = kPackedP<N>>
 struct SolveSmem {
