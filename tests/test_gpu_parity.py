@@ -75,6 +75,28 @@ def test_newton_method_matches(cuda):
     _check_against_oracle(params, batch.x0, batch.ref, batch.u_prev, out, range(0, 256, 5))
 
 
+@pytest.mark.parametrize("cfg,N,B", [("config2", 20, 1024), ("config3", 10, 1024), ("config3", 24, 1024),
+                                     ("config3", 31, 1024), ("config4", 30, 4096)])
+def test_iteration_indexing_bit_exact_on_product_path(cuda, cfg, N, B):
+    """The product kernel (fast mode) against the C restatement on whole batches: all four counters
+    (ADMM iterations, polish passes, factorizations, line-search trials), statuses and active sets
+    identical on every QP -- the north star's bit-exact iteration / active-set indexing."""
+    import cpu_solver
+    from mpcqp import scenarios
+
+    batch = {"config2": lambda: scenarios.config2(B),
+             "config3": lambda: scenarios.config3(B, horizon=N, seed=5000 + N),
+             "config4": lambda: scenarios.config4(B)}[cfg]()
+    params = _params(batch.horizon)
+    out = _solve(params, batch.x0, batch.ref, batch.u_prev)
+    ref = cpu_solver.cpu_solve(params, batch.x0, batch.ref, batch.u_prev)
+    same = (out["iters"] == ref["iters"]).all(axis=1)
+    assert same.all(), f"QPs {np.flatnonzero(~same)[:10]} disagree on iteration counts"
+    assert np.array_equal(out["status"], ref["status"])
+    assert np.array_equal(out["active"], ref["active"])
+    assert _rel(out["U"], ref["U"]) <= REL_TOL
+
+
 @pytest.mark.parametrize("schedule", [
     {},                                       # the default polish schedule (early + near-tolerance)
     {"polish_near": 0.0},                     # early polish from iteration 150 only
@@ -92,9 +114,11 @@ def test_iteration_counts_match_cpu_restatement(cuda, schedule):
     ref = cpu_solver.cpu_solve(params, batch.x0, batch.ref, batch.u_prev, **schedule)
     assert (out["status"] == 1).all()
     same = (out["iters"] == ref["iters"]).all(axis=1)
-    # rounding differs (wavefront tree reductions vs sequential sums); the iteration
-    # counts must agree for the overwhelming majority and the solutions for all
-    assert same.mean() >= 0.95, f"only {same.mean():.3f} of QPs agree on iteration counts"
+    # bit-exact iteration indexing on the product path: the wavefront tree reductions round
+    # differently from the C code's sequential sums, but no counter decision flips on these QPs
+    # (profiles/r03_s4_iters_agreement.json: 100 % over 46k QPs of configs 2/3/4 and N = 1..31)
+    assert same.all(), f"QPs {np.flatnonzero(~same)[:10]} disagree on iteration counts"
+    assert np.array_equal(out["status"], ref["status"])
     assert np.array_equal(out["active"], ref["active"])
     assert _rel(out["U"], ref["U"]) <= REL_TOL
 

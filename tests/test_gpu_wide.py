@@ -8,8 +8,8 @@ and sums its line search in tree order.  Checks:
   * the exact oracle (mpc_oracle.solve_exact): U / X / u0 to 1e-8 relative, identical active sets;
   * reproducible = 1 against the C restatement fed the GPU's own LTV model (K1 output): U, X,
     statuses AND iteration counts identical bit for bit;
-  * the fast mode against the same: statuses and active sets identical, U to 1e-8, ADMM
-    iterations identical and all four counters on >= 95 % of QPs;
+  * the fast mode against the same: statuses, active sets and all four counters identical on
+    every QP, U to 1e-8;
   * the drop-in surface: MPCController(MPCConfig(horizon=40)) and a fleet at N = 40;
   * horizons past a wave (N = 64..127): K1 in chunks of 64 rows, the sweep in memory past 2N = 128.
 """
@@ -94,8 +94,9 @@ def test_long_horizons_bit_exact_with_c_restatement(cuda, N, settings):
 
 @pytest.mark.parametrize("N,settings", [(32, {}), (40, {}), (48, {"polish_from": 0, "polish_near": 0.0}), (63, {})])
 def test_long_horizons_fast_mode_against_c_restatement(cuda, N, settings):
-    """The default (fast) long-horizon mode: the same optimum and statuses as the C restatement,
-    the same ADMM run (its arithmetic is unchanged), rank-1 polish counters on >= 95 % of QPs."""
+    """The default (fast) long-horizon mode (the mid kernel): the same optimum, statuses, active sets
+    and all four counters as the C restatement on every QP (its tree-order sums round differently,
+    but no counter decision flips: profiles/r03_s4_iters_agreement.json, 6 x 1024 QPs at N = 32..63)."""
     import cpu_solver
     from mpcqp import scenarios
 
@@ -106,9 +107,8 @@ def test_long_horizons_fast_mode_against_c_restatement(cuda, N, settings):
     assert np.array_equal(out["status"], ref["status"])
     assert np.array_equal(out["active"], ref["active"])
     assert _rel(out["U"], ref["U"]) <= REL_TOL and _rel(out["X"], ref["X"]) <= REL_TOL
-    same = (out["iters"] == ref["iters"]).all(axis=1).mean()
-    assert same >= 0.95, same
-    assert (out["iters"][:, 0] == ref["iters"][:, 0]).mean() >= 0.95
+    same = (out["iters"] == ref["iters"]).all(axis=1)
+    assert same.all(), f"QPs {np.flatnonzero(~same)[:10]} disagree on iteration counts"
 
 
 @pytest.mark.parametrize("N,config,settings", [(1, "config3", {}), (5, "config3", {}), (10, "config3", {}),

@@ -1,8 +1,8 @@
 #!/usr/bin/env python3
 """Iteration indexing of the product path: the fraction of QPs whose four counters (ADMM
 iterations, polish passes, factorizations, line-search trials), status and active set equal the C
-restatement's (oracle/mpcqp_cpu.c), over the BASELINE configs at full size and config 3 at every
-one-wave horizon.  Writes one JSON object (profiles/r03_*_iters_agreement.json).
+restatement's (oracle/mpcqp_cpu.c), over the BASELINE configs at full size, config 3 at the
+one-wave horizons and at mid horizons.  Writes one JSON object (profiles/r03_*_iters_agreement.json).
 
     python tools/iters_agreement.py [--quick]
 """
@@ -62,6 +62,9 @@ def main() -> None:
             ("config4_B16384_N30", lambda: scenarios.config4(2048 if a.quick else 16384), {})]
     for N in ([5, 10, 31] if a.quick else [1, 2, 3, 5, 8, 10, 12, 15, 18, 21, 24, 26, 28, 29, 30, 31]):
         runs.append((f"config3_B1024_N{N}", (lambda N=N: scenarios.config3(1024, horizon=N, seed=5000 + N)), {}))
+    # the mid-horizon kernel (N = 32..63, k_solve_mid)
+    for N in ([40] if a.quick else [32, 36, 40, 48, 56, 63]):
+        runs.append((f"config3_B1024_N{N}_mid", (lambda N=N: scenarios.config3(1024, horizon=N, seed=5000 + N)), {}))
     for name, mk, settings in runs:
         b = mk()
         out["runs"][name] = agreement(P(b.horizon), b, **settings)
