@@ -365,6 +365,13 @@ int mpcqp_swarm_step(mpcqp_ws* nominal, mpcqp_ws* relaxed, const mpcqp_fleet* f,
 int mpcqp_swarm_run(mpcqp_ws* nominal, mpcqp_ws* relaxed, const mpcqp_fleet* f, const mpcqp_swarm* s, int steps,
                     int use_graph, void* stream);
 
+/* The whole swarm run (every vehicle to its goal, abort or max_steps) as max_replans + 1 launches of
+ * the fused fleet loop (mpcqp_fleet_loop) with the replan trigger inside -- a vehicle leaves its loop
+ * when the trigger fires -- and the replanning kernels between them (ABI 6).  The same operations per
+ * vehicle as mpcqp_swarm_run to the end, so every fleet and swarm output buffer equals it bit for bit.
+ * Parameter blocks without the fused kernel run mpcqp_swarm_run(max_steps, graph). */
+int mpcqp_swarm_loop(mpcqp_ws* nominal, mpcqp_ws* relaxed, const mpcqp_fleet* f, const mpcqp_swarm* s, void* stream);
+
 /*
  * Occupancy inflation: src/maps/inflate.py:18-51 (the fallback
  * dilation the reference uses without OpenCV) for B grids of height x width uint8

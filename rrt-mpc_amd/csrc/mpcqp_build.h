@@ -164,6 +164,11 @@ __device__ __forceinline__ bool fleet_off_row(double x, double y, const double* 
   const double dy = y - r[1];
   return dx * dx + dy * dy > 25.0;
 }
+// the config-5 off-track trigger (README.md:146-148): farther than d from ref row r
+__device__ __forceinline__ bool swarm_off_track(double x, double y, const double* r, double d) {
+#pragma clang fp contract(off)
+  return hypot(x - r[0], y - r[1]) > d;
+}
 // goal test (control_stage.py:147-150)
 __device__ __forceinline__ bool fleet_at_goal(double x, double y, double gx, double gy) {
 #pragma clang fp contract(off)

@@ -283,9 +283,18 @@ template <int N>
 void launch_solve(hipStream_t s, const Launch& L);
 // the fused closed loop of a fleet (k_fleet_loop<N>, mpcqp_solve.h; N <= 31, fast mode): `steps`
 // loop steps of every RUNNING vehicle in one launch
+// The config-5 replan trigger inside the fused loop (mpcqp_swarm_loop): after each step a RUNNING
+// vehicle farther than replan_distance from ref[path_idx], or an ABORTED one, with replans left leaves
+// the loop as MPCQP_FLEET_REPLAN_* with its replanning problem in start_goal.  max_replans = 0: off.
+struct LoopTrigger {
+  double replan_distance;
+  int max_replans;
+  const int32_t* replans;
+  double* start_goal;
+};
 template <int N>
-void launch_fleet_loop(hipStream_t s, const mpcqp_params* P, const mpcqp_fleet& f, int steps);
-typedef void (*fleet_loop_t)(hipStream_t, const mpcqp_params*, const mpcqp_fleet&, int);
+void launch_fleet_loop(hipStream_t s, const mpcqp_params* P, const mpcqp_fleet& f, int steps, const LoopTrigger& tr);
+typedef void (*fleet_loop_t)(hipStream_t, const mpcqp_params*, const mpcqp_fleet&, int, const LoopTrigger&);
 // nullptr when the parameter block does not run the one-wave kernel; defined in mpcqp.hip
 fleet_loop_t fleet_looper(const mpcqp_params& p);
 // the long-horizon solve (N >= MPCQP_WIDE_MIN_HORIZON; mpcqp_wide.hip): one 256-thread workgroup
@@ -324,3 +333,10 @@ struct mpcqp_ws {
   // run-time-selected argument block to scratch); written by a kernel on the launch stream
   mpcqp_params* dparams;
 };
+
+namespace mpcqp {
+// the fused fleet loop (mpcqp_fleet.hip), with the swarm's trigger when tr.max_replans > 0; *fused =
+// false (nothing enqueued) when the parameter blocks do not run the one-wave kernel
+int enqueue_fleet_loop(mpcqp_ws* nominal, mpcqp_ws* relaxed, const mpcqp_fleet* f, int steps, const LoopTrigger& tr,
+                       hipStream_t s, bool* fused);
+}  // namespace mpcqp

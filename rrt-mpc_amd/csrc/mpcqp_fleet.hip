@@ -214,24 +214,40 @@ int mpcqp_fleet_step(mpcqp_ws* nominal, mpcqp_ws* relaxed, const mpcqp_fleet* f,
   return enqueue_step(nominal, relaxed, f, static_cast<hipStream_t>(stream));
 }
 
+}  // extern "C"
+
+namespace mpcqp {
+// the fused loop with the swarm's trigger (tr.max_replans > 0, mpcqp_swarm_loop) or without; nullptr
+// looper (mid / long horizons, reproducible or debug mode): *fused = false, nothing enqueued
+int enqueue_fleet_loop(mpcqp_ws* nominal, mpcqp_ws* relaxed, const mpcqp_fleet* f, int steps, const LoopTrigger& tr,
+                       hipStream_t s, bool* fused) {
+  const mpcqp::fleet_loop_t loop = mpcqp::fleet_looper(nominal->p);
+  *fused = loop && mpcqp::fleet_looper(relaxed->p) == loop;
+  if (!*fused) return MPCQP_OK;
+  nominal->built_B = -1;  // as mpcqp_fleet_step: a later mpcqp_solve needs its own build
+  relaxed->built_B = -1;
+  nominal->in_x0 = nominal->in_ref = nominal->in_up = nullptr;
+  relaxed->in_x0 = relaxed->in_ref = relaxed->in_up = nullptr;
+  hipLaunchKernelGGL(k_store_params, dim3(1), dim3(kWave), 0, s, nominal->p, relaxed->p, nominal->dparams);
+  loop(s, nominal->dparams, *f, steps, tr);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return fail(MPCQP_E_HIP, std::string("k_fleet_loop launch: ") + hipGetErrorString(e));
+  return MPCQP_OK;
+}
+}  // namespace mpcqp
+
+extern "C" {
+
 int mpcqp_fleet_loop(mpcqp_ws* nominal, mpcqp_ws* relaxed, const mpcqp_fleet* f, int steps, void* stream) {
   int rc = check_fleet(nominal, relaxed, f);
   if (rc) return rc;
   if (steps < 0) return fail(MPCQP_E_ARG, "steps must be >= 0");
   if (f->vehicles == 0 || steps == 0) return MPCQP_OK;
   hipStream_t s = static_cast<hipStream_t>(stream);
-  const mpcqp::fleet_loop_t loop = mpcqp::fleet_looper(nominal->p);
-  if (!loop || mpcqp::fleet_looper(relaxed->p) != loop)  // mid / long horizons, reproducible or debug mode
-    return run_graph(nominal, relaxed, f, steps, s);
-  nominal->built_B = -1;  // as mpcqp_fleet_step: a later mpcqp_solve needs its own build
-  relaxed->built_B = -1;
-  nominal->in_x0 = nominal->in_ref = nominal->in_up = nullptr;
-  relaxed->in_x0 = relaxed->in_ref = relaxed->in_up = nullptr;
-  hipLaunchKernelGGL(k_store_params, dim3(1), dim3(kWave), 0, s, nominal->p, relaxed->p, nominal->dparams);
-  loop(s, nominal->dparams, *f, steps);
-  hipError_t e = hipGetLastError();
-  if (e != hipSuccess) return fail(MPCQP_E_HIP, std::string("k_fleet_loop launch: ") + hipGetErrorString(e));
-  return MPCQP_OK;
+  bool fused = false;
+  rc = mpcqp::enqueue_fleet_loop(nominal, relaxed, f, steps, mpcqp::LoopTrigger{0.0, 0, nullptr, nullptr}, s, &fused);
+  if (rc || fused) return rc;
+  return run_graph(nominal, relaxed, f, steps, s);  // mid / long horizons, reproducible or debug mode
 }
 
 int mpcqp_fleet_run(mpcqp_ws* nominal, mpcqp_ws* relaxed, const mpcqp_fleet* f, int steps, int use_graph,

@@ -1564,7 +1564,8 @@ __global__ __launch_bounds__(kWave, kSolveWavesPerEU<N>) void k_solve(mpcqp_para
 // in LDS across steps (no registers held through the solve); it is written back at the end.
 template <int N>
 __global__ __launch_bounds__(kWave, kSolveWavesPerEU<N>) void k_fleet_loop(const mpcqp_params* __restrict__ P,
-                                                                         mpcqp_fleet f, int steps) {
+                                                                         mpcqp_fleet f, int steps,
+                                                                         mpcqp::LoopTrigger tr) {
   __shared__ SolveLds<N> sm;
   __shared__ double ls[6];  // loop state: x[4], u_prev[2]
   const int b = blockIdx.x;
@@ -1572,7 +1573,24 @@ __global__ __launch_bounds__(kWave, kSolveWavesPerEU<N>) void k_fleet_loop(const
   const int V = f.vehicles;
   if (b >= V) return;
   int phase = f.phase[b];
-  if (phase != MPCQP_FLEET_RUNNING) return;
+  // the swarm's trigger (mpcqp_swarm_loop): replans left for this vehicle
+  const bool can_replan = tr.max_replans > 0 && tr.replans[b] >= 0 && tr.replans[b] < tr.max_replans;
+  auto to_replan = [&](int ph, double x, double y) {  // k_swarm_trigger's transition and problem
+    if (lane == 0) {
+      f.phase[b] = ph == MPCQP_FLEET_ABORTED ? MPCQP_FLEET_REPLAN_ABORTED : MPCQP_FLEET_REPLAN_RUNNING;
+      double* sg = tr.start_goal + 4 * (size_t)b;
+      sg[0] = x;
+      sg[1] = y;
+      sg[2] = f.goal[(size_t)b * 2];
+      sg[3] = f.goal[(size_t)b * 2 + 1];
+    }
+  };
+  if (phase != MPCQP_FLEET_RUNNING) {
+    // an ABORTED vehicle with replans left is replanned before it steps again (the stepped swarm's
+    // trigger fires for it in every step)
+    if (phase == MPCQP_FLEET_ABORTED && can_replan) to_replan(phase, f.state[(size_t)b * 4], f.state[(size_t)b * 4 + 1]);
+    return;
+  }
   const int len = f.ref_len[b];
   int pidx = f.path_idx[b];
   int k = f.steps[b];
@@ -1643,6 +1661,12 @@ __global__ __launch_bounds__(kWave, kSolveWavesPerEU<N>) void k_fleet_loop(const
       phase = MPCQP_FLEET_OUT_OF_STEPS;
       break;
     }
+    // k_swarm_trigger after the step: off the reference (state and path_idx after the step)
+    if (can_replan && tr.replan_distance > 0.0 && len >= 1 && len <= f.ref_stride && pidx >= 0 && pidx < len &&
+        swarm_off_track(xn[0], xn[1], rows + (size_t)pidx * 4, tr.replan_distance)) {
+      phase = MPCQP_FLEET_REPLAN_RUNNING;
+      break;
+    }
   }
   if (lane < 4) f.state[(size_t)b * 4 + lane] = ls[lane];
   else if (lane < 6) f.u_prev[(size_t)b * 2 + lane - 4] = ls[lane];
@@ -1650,6 +1674,10 @@ __global__ __launch_bounds__(kWave, kSolveWavesPerEU<N>) void k_fleet_loop(const
     f.path_idx[b] = pidx;
     f.steps[b] = k;
     f.phase[b] = phase;
+  }
+  if ((phase == MPCQP_FLEET_ABORTED && can_replan) || phase == MPCQP_FLEET_REPLAN_RUNNING) {
+    __syncthreads();
+    to_replan(phase, ls[0], ls[1]);
   }
 }
 
@@ -1663,8 +1691,8 @@ void launch_solve(hipStream_t s, const Launch& L) {
                      L.st, L.it, L.ac);
 }
 template <int N>
-void launch_fleet_loop(hipStream_t s, const mpcqp_params* P, const mpcqp_fleet& f, int steps) {
-  hipLaunchKernelGGL(k_fleet_loop<N>, dim3(f.vehicles), dim3(kWave), 0, s, P, f, steps);
+void launch_fleet_loop(hipStream_t s, const mpcqp_params* P, const mpcqp_fleet& f, int steps, const LoopTrigger& tr) {
+  hipLaunchKernelGGL(k_fleet_loop<N>, dim3(f.vehicles), dim3(kWave), 0, s, P, f, steps, tr);
 }
 
 }  // namespace mpcqp

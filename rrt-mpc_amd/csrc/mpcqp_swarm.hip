@@ -18,6 +18,10 @@
 //                       ABORTED; either way one replan is used
 // Every replanning kernel exits at once for an unflagged vehicle, so a step without replans
 // costs a handful of empty launches; mpcqp_swarm_run replays the whole step as a hipGraph.
+// mpcqp_swarm_loop runs the same thing as max_replans + 1 launches of the fused fleet loop
+// (k_fleet_loop with the trigger: each vehicle steps until it triggers or ends) with the replanning
+// kernels in between -- no per-step launches.
+#include "mpcqp_build.h"
 #include "mpcqp_plan.h"
 #include "mpcqp_refbuild.h"
 
@@ -42,8 +46,8 @@ __global__ __launch_bounds__(kWave) void k_swarm_trigger(mpcqp_fleet f, mpcqp_sw
   if (ph == MPCQP_FLEET_RUNNING && s.replan_distance > 0.0) {
     const int len = f.ref_len[v], pi = f.path_idx[v];
     if (len >= 1 && len <= f.ref_stride && pi >= 0 && pi < len) {
-      const double* r = f.ref_global + ((size_t)v * f.ref_stride + pi) * 4;
-      go = hypot(f.state[(size_t)v * 4] - r[0], f.state[(size_t)v * 4 + 1] - r[1]) > s.replan_distance;
+      go = swarm_off_track(f.state[(size_t)v * 4], f.state[(size_t)v * 4 + 1],
+                           f.ref_global + ((size_t)v * f.ref_stride + pi) * 4, s.replan_distance);
     }
   }
   if (!go) return;
@@ -208,14 +212,15 @@ int set_replan_attrs(const mpcqp_swarm* s) {
   return MPCQP_OK;
 }
 
-int enqueue_replan(const mpcqp_fleet* f, const mpcqp_swarm* s, hipStream_t st) {
+// trigger (unless the fused loop already flagged the vehicles) + the replanning kernels
+int enqueue_replan(const mpcqp_fleet* f, const mpcqp_swarm* s, hipStream_t st, bool trigger = true) {
   const int V = f->vehicles;
   if (s->max_replans == 0 || V == 0) return MPCQP_OK;
   const mpcqp_fleet fv = *f;
   const mpcqp_swarm sv = *s;
   const ReplanLds l(s);
   const size_t lp = l.plan, lx = l.paths, lc = l.smooth, lr = l.refbuild;
-  hipLaunchKernelGGL(k_swarm_trigger, dim3((V + kWave - 1) / kWave), dim3(kWave), 0, st, fv, sv);
+  if (trigger) hipLaunchKernelGGL(k_swarm_trigger, dim3((V + kWave - 1) / kWave), dim3(kWave), 0, st, fv, sv);
   hipLaunchKernelGGL(k_swarm_plan, dim3(V), dim3(kPlanThreads), lp, st, fv, sv);
   hipLaunchKernelGGL(k_swarm_paths, dim3(V), dim3(kPlanThreads), lx, st, fv, sv);
   hipLaunchKernelGGL(k_swarm_smooth, dim3(V), dim3(kWave), lc, st, fv, sv);
@@ -261,6 +266,28 @@ int mpcqp_swarm_step(mpcqp_ws* nominal, mpcqp_ws* relaxed, const mpcqp_fleet* f,
     if (rc) return rc;
   }
   return enqueue_replan(f, s, st);
+}
+
+int mpcqp_swarm_loop(mpcqp_ws* nominal, mpcqp_ws* relaxed, const mpcqp_fleet* f, const mpcqp_swarm* s, void* stream) {
+  int rc = check_swarm(f, s);
+  if (rc) return rc;
+  rc = mpcqp_fleet_loop(nominal, relaxed, f, 0, stream);  // the fleet's checks (no work at 0 steps)
+  if (rc) return rc;
+  if (f->vehicles == 0) return MPCQP_OK;
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  if (s->max_replans > 0 && (rc = set_replan_attrs(s)) != MPCQP_OK) return rc;
+  // max_replans + 1 rounds: every vehicle runs until it triggers or ends, the flagged ones are
+  // replanned; a vehicle's r-th trigger comes in round r - 1, so the last round triggers none
+  const mpcqp::LoopTrigger tr{s->replan_distance, s->max_replans, s->replans, s->start_goal};
+  for (int r = 0; r <= s->max_replans; ++r) {
+    bool fused = false;
+    rc = mpcqp::enqueue_fleet_loop(nominal, relaxed, f, f->max_steps, tr, st, &fused);
+    if (rc) return rc;
+    if (!fused)  // mid / long horizons, reproducible or debug mode: the stepped swarm to the end
+      return mpcqp_swarm_run(nominal, relaxed, f, s, f->max_steps, 1, stream);
+    if (r < s->max_replans && (rc = enqueue_replan(f, s, st, false)) != MPCQP_OK) return rc;
+  }
+  return MPCQP_OK;
 }
 
 int mpcqp_swarm_run(mpcqp_ws* nominal, mpcqp_ws* relaxed, const mpcqp_fleet* f, const mpcqp_swarm* s, int steps,

@@ -247,6 +247,8 @@ _SYMBOLS = {
                           ctypes.c_void_p], ctypes.c_int),
     "mpcqp_swarm_run": ([ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(MpcqpFleet), ctypes.POINTER(MpcqpSwarm),
                          ctypes.c_int, ctypes.c_int, ctypes.c_void_p], ctypes.c_int),
+    "mpcqp_swarm_loop": ([ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(MpcqpFleet), ctypes.POINTER(MpcqpSwarm),
+                          ctypes.c_void_p], ctypes.c_int),
     "mpcqp_model_buffer": ([ctypes.c_void_p], ctypes.c_void_p),
     "mpcqp_model_stride": ([ctypes.c_int], ctypes.c_int),
     "mpcqp_state_buffer": ([ctypes.c_void_p], ctypes.c_void_p),

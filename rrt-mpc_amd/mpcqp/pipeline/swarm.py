@@ -13,7 +13,9 @@ on the GPU with a per-step replan trigger.
                where it stands (RRT* with its next seed ``seed + 7919 (r + 1)``, pruning,
                smoothing, build_reference); pose, speed and u_prev carry over, path_idx restarts at
                0.  At most ``max_replans`` per vehicle.  The whole step is one hipGraph replay; the
-               host only polls every ``check_every`` steps whether any vehicle still runs.
+               host only polls every ``check_every`` steps whether any vehicle still runs.  With
+               ``fused=True``: ``mpcqp_swarm_loop``, the fused fleet loop with the trigger inside
+               (max_replans + 1 launches, the replanning kernels between them).
 Every vehicle between replans follows the reference's single-vehicle loop exactly.
 """
 from __future__ import annotations
@@ -56,7 +58,7 @@ class SwarmResult:
 class Swarm:
     def __init__(self, occupancy: np.ndarray, mpc, planner: PlannerParameters, *, map_resolution: float,
                  max_vehicles: int, max_ref_len: int = 512, device=None, replan_distance: float = 15.0,
-                 max_replans: int = 2, path_cap: int = 6144, use_graph: bool = True) -> None:
+                 max_replans: int = 2, path_cap: int = 6144, use_graph: bool = True, fused: bool = False) -> None:
         # path_cap: smoothed points a replan may produce.  The default is the most that the device
         # reference builder stages (kRefCap, csrc/mpcqp_swarm.hip), so a replanned path is never cut
         # shorter than a reference could be built from; capacity failures are reported apart from
@@ -71,6 +73,9 @@ class Swarm:
         self.max_replans = int(max_replans)
         self.path_cap = int(path_cap)
         self.use_graph = bool(use_graph)
+        # fused: the run as max_replans + 1 launches of the fused fleet loop with the trigger inside
+        # (mpcqp_swarm_loop) instead of one graph-replayed launch sequence per step
+        self.fused = bool(fused)
         self._L = _lib.lib()
 
     def _plan(self, starts, goals, seeds):
@@ -155,6 +160,11 @@ class Swarm:
         t0 = time.perf_counter()
         stream = torch.cuda.current_stream(self.device)
         done = 0
+        if self.fused and V:
+            _lib.check(self._L.mpcqp_swarm_loop(self.fleet._nominal._ws, self.fleet._relaxed._ws,
+                                                ctypes.byref(self.fleet._fleet), ctypes.byref(sw),
+                                                ctypes.c_void_p(stream.cuda_stream)), "mpcqp_swarm_loop")
+            done = total
         while done < total and V:
             k = min(check_every, total - done)
             _lib.check(self._L.mpcqp_swarm_run(self.fleet._nominal._ws, self.fleet._relaxed._ws,

@@ -268,3 +268,26 @@ def test_sharded_swarm_equals_one_swarm(cuda, golden):
     np.testing.assert_array_equal(got.replans, one.replans)
     np.testing.assert_array_equal(got.planned, one.planned)
     assert all(np.array_equal(a, b) for a, b in zip(got.states, one.states))
+
+
+@pytest.mark.parametrize("V,steps,dist,max_replans,seed", [(100, 150, 5.5, 1, 7), (40, 200, 2.5, 2, 21),
+                                                           (64, 120, 1.5, 3, 33)])
+def test_fused_swarm_equals_stepped_swarm(cuda, golden, V, steps, dist, max_replans, seed):
+    """mpcqp_swarm_loop (max_replans + 1 fused-loop launches, the trigger inside the loop) == the
+    graph-stepped swarm (mpcqp_swarm_run): every vehicle's states, inputs, phase, steps, replans,
+    replan steps, replan start and new plan identical bit for bit, with the trigger firing."""
+    starts, goals = _pairs(golden("default_plan.npz")["occupancy"], V, seed)
+    occ = golden("default_plan.npz")["occupancy"]
+    res = [_swarm(occ, V, steps, replan_distance=dist, max_replans=max_replans, fused=fused)
+           .run(starts, goals, seeds=np.arange(V), check_every=25) for fused in (False, True)]
+    a, b = res
+    assert a.replans.sum() > 0, "the trigger should fire"
+    for k in ("steps", "phase", "replans", "planned", "replan_steps", "last_replan_start"):
+        np.testing.assert_array_equal(getattr(a, k), getattr(b, k), err_msg=k)
+    for v in range(V):
+        np.testing.assert_array_equal(a.states[v], b.states[v])
+        np.testing.assert_array_equal(a.inputs[v], b.inputs[v])
+        pa, pb = a.last_replan_path[v], b.last_replan_path[v]
+        assert (pa is None) == (pb is None)
+        if pa is not None:
+            np.testing.assert_array_equal(pa, pb)

@@ -65,7 +65,7 @@ def distributed(a) -> None:
         starts, goals = pairs(occ, V, 5)
         lo, hi = shard_vehicles(V, world, rank)
         sw = Swarm(occ, mpc, prm, map_resolution=0.8, max_vehicles=max(hi - lo, 1), device=dev,
-                   replan_distance=a.replan_distance, max_replans=a.max_replans)
+                   replan_distance=a.replan_distance, max_replans=a.max_replans, fused=a.fused)
         sw.run(starts[:1], goals[:1], seeds=np.arange(1), sim_steps=5)  # warm
         torch.cuda.synchronize(dev)
         dist.barrier()
@@ -104,6 +104,8 @@ def main() -> None:
                     help="per-step off-track trigger (px); the default fires for a share of the vehicles")
     ap.add_argument("--max-replans", type=int, default=2)
     ap.add_argument("--distributed", action="store_true", help="vehicles sharded over torch.distributed ranks")
+    ap.add_argument("--fused", action="store_true",
+                    help="mpcqp_swarm_loop: the fused fleet loop with the trigger inside (max_replans + 1 launches)")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"])
     a = ap.parse_args()
     if a.distributed:
@@ -123,7 +125,7 @@ def main() -> None:
     for V in a.vehicles:
         starts, goals = pairs(occ, V, 5)
         sw = Swarm(occ, MPCConfig(horizon=15, sim_steps=a.steps), prm, map_resolution=0.8, max_vehicles=V,
-                   device="cuda:0", replan_distance=a.replan_distance, max_replans=a.max_replans)
+                   device="cuda:0", replan_distance=a.replan_distance, max_replans=a.max_replans, fused=a.fused)
         sw.run(starts[:4], goals[:4], seeds=np.arange(4), sim_steps=5)  # warm
         torch.cuda.synchronize()
         t0 = time.perf_counter()
@@ -131,7 +133,8 @@ def main() -> None:
         torch.cuda.synchronize()
         dt = time.perf_counter() - t0
         ok_replans = int((res.replan_steps > 0).sum())
-        run = {"vehicles": V, "seconds": dt, "vehicle_steps": int(res.steps.sum()),
+        run = {"vehicles": V, "mode": "fused loop (mpcqp_swarm_loop)" if a.fused else "graph-stepped (mpcqp_swarm_run)",
+               "seconds": dt, "vehicle_steps": int(res.steps.sum()),
                "vehicle_steps_per_s": int(res.steps.sum()) / dt,
                "planned": int(res.planned.sum()), "goal_reached": int((res.phase == 1).sum()),
                "replans": int(res.replans.sum()), "replans_with_new_plan": ok_replans,
