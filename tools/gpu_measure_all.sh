@@ -14,5 +14,6 @@ done &&
 timeout -k 10 300 python -u tools/fleet_bench.py > $O/fleet_bench.json 2> $O/fleet_bench.err &&
 timeout -k 10 300 python -u tools/fleet_bench.py --fused > $O/fleet_bench_fused.json 2> $O/fleet_bench_fused.err &&
 timeout -k 10 500 python -u tools/iters_agreement.py > $O/iters_agreement.json 2> $O/iters_agreement.err &&
-timeout -k 10 300 python -u tools/swarm_bench.py > $O/swarm_bench.json 2> $O/swarm_bench.err
+timeout -k 10 300 python -u tools/swarm_bench.py > $O/swarm_bench.json 2> $O/swarm_bench.err &&
+timeout -k 10 300 python -u tools/swarm_bench.py --fused > $O/swarm_bench_fused.json 2> $O/swarm_bench_fused.err
 echo "exit $?"
