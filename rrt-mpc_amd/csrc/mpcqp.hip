@@ -187,14 +187,17 @@ int mpcqp_create(const mpcqp_params* p, int max_batch, int device, mpcqp_ws** ws
   w->state = nullptr;
   w->in_x0 = w->in_ref = w->in_up = nullptr;
   w->dparams = nullptr;
+  w->dorder = nullptr;
   const size_t mbytes = sizeof(double) * (size_t)model_stride(p->horizon) * (size_t)max_batch;
   const size_t sbytes = sizeof(double) * ws_state_stride(p->horizon, mpcqp::wide_solve(*p)) * (size_t)max_batch;
   e = hipMalloc(&w->model, mbytes);
   if (e == hipSuccess) e = hipMalloc(&w->state, sbytes);
   if (e == hipSuccess) e = hipMalloc(&w->dparams, 2 * sizeof(mpcqp_params));
+  if (e == hipSuccess) e = hipMalloc(&w->dorder, sizeof(int32_t) * (size_t)max_batch);
   if (e != hipSuccess) {
     if (w->model) (void)hipFree(w->model);
     if (w->state) (void)hipFree(w->state);
+    if (w->dparams) (void)hipFree(w->dparams);
     delete w;
     return fail(MPCQP_E_HIP, std::string("hipMalloc: ") + hipGetErrorString(e));
   }
@@ -224,6 +227,7 @@ void mpcqp_destroy(mpcqp_ws* ws) {
   (void)hipFree(ws->model);
   (void)hipFree(ws->state);
   (void)hipFree(ws->dparams);
+  (void)hipFree(ws->dorder);
   delete ws;
 }
 

@@ -291,6 +291,10 @@ struct LoopTrigger {
   int max_replans;
   const int32_t* replans;
   double* start_goal;
+  // workgroup -> vehicle (nullptr: identity).  The fused loops dispatch the vehicles longest
+  // reference first: a vehicle's step count follows its reference length, and the slowest
+  // vehicles started last would set the run's tail once the vehicles outnumber the wave slots.
+  const int32_t* order = nullptr;
 };
 template <int N>
 void launch_fleet_loop(hipStream_t s, const mpcqp_params* P, const mpcqp_fleet& f, int steps, const LoopTrigger& tr);
@@ -332,6 +336,8 @@ struct mpcqp_ws {
   // loop selects its block per solve, which a kernel argument cannot be (the compiler copies a
   // run-time-selected argument block to scratch); written by a kernel on the launch stream
   mpcqp_params* dparams;
+  // the fused loop's dispatch order (max_batch vehicles), written by k_fleet_order on the stream
+  int32_t* dorder;
 };
 
 namespace mpcqp {

@@ -123,6 +123,36 @@ __global__ __launch_bounds__(kWave) void k_store_params(mpcqp_params pn, mpcqp_p
   }
 }
 
+// The fused loop's dispatch order: the vehicles by reference length, longest first (a bucket sort
+// on the length, 1024 buckets; the order inside a bucket is immaterial -- vehicles are independent).
+// One 1024-thread workgroup.
+constexpr int kOrderBuckets = 1024;
+__global__ __launch_bounds__(kOrderBuckets) void k_fleet_order(mpcqp_fleet f, int32_t* __restrict__ order) {
+  __shared__ int cnt[kOrderBuckets];
+  const int t = threadIdx.x, V = f.vehicles;
+  const int span = f.ref_stride + 1;
+  auto bucket = [&](int v) {
+    int len = f.ref_len[v];
+    len = len < 0 ? 0 : (len > f.ref_stride ? f.ref_stride : len);
+    return (int)(((long long)(f.ref_stride - len) * kOrderBuckets) / span);  // longest -> bucket 0
+  };
+  cnt[t] = 0;
+  __syncthreads();
+  for (int v = t; v < V; v += kOrderBuckets) atomicAdd(&cnt[bucket(v)], 1);
+  __syncthreads();
+  for (int d = 1; d < kOrderBuckets; d <<= 1) {  // inclusive scan (Hillis-Steele)
+    const int add = t >= d ? cnt[t - d] : 0;
+    __syncthreads();
+    cnt[t] += add;
+    __syncthreads();
+  }
+  const int excl = t ? cnt[t - 1] : 0;
+  __syncthreads();
+  cnt[t] = excl;
+  __syncthreads();
+  for (int v = t; v < V; v += kOrderBuckets) order[atomicAdd(&cnt[bucket(v)], 1)] = v;
+}
+
 int check_fleet(const mpcqp_ws* nom, const mpcqp_ws* rel, const mpcqp_fleet* f) {
   if (!nom || !rel || !f) return fail(MPCQP_E_ARG, "null argument");
   if (nom == rel) return fail(MPCQP_E_ARG, "nominal and relaxed workspaces must differ");
@@ -229,7 +259,16 @@ int enqueue_fleet_loop(mpcqp_ws* nominal, mpcqp_ws* relaxed, const mpcqp_fleet* 
   nominal->in_x0 = nominal->in_ref = nominal->in_up = nullptr;
   relaxed->in_x0 = relaxed->in_ref = relaxed->in_up = nullptr;
   hipLaunchKernelGGL(k_store_params, dim3(1), dim3(kWave), 0, s, nominal->p, relaxed->p, nominal->dparams);
-  loop(s, nominal->dparams, *f, steps, tr);
+  LoopTrigger tro = tr;
+  // longest first only when the vehicles outnumber the wave slots (2 per SIMD): with every vehicle
+  // resident at once the order only changes which vehicles share a SIMD (measured: no gain)
+  int cus = 0;
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, nominal->device) != hipSuccess) cus = 0;
+  if (cus > 0 && f->vehicles > 8 * cus) {
+    hipLaunchKernelGGL(k_fleet_order, dim3(1), dim3(kOrderBuckets), 0, s, *f, nominal->dorder);
+    tro.order = nominal->dorder;
+  }
+  loop(s, nominal->dparams, *f, steps, tro);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return fail(MPCQP_E_HIP, std::string("k_fleet_loop launch: ") + hipGetErrorString(e));
   return MPCQP_OK;

@@ -1568,7 +1568,7 @@ __global__ __launch_bounds__(kWave, kSolveWavesPerEU<N>) void k_fleet_loop(const
                                                                          mpcqp::LoopTrigger tr) {
   __shared__ SolveLds<N> sm;
   __shared__ double ls[6];  // loop state: x[4], u_prev[2]
-  const int b = blockIdx.x;
+  const int b = tr.order ? tr.order[blockIdx.x] : (int)blockIdx.x;
   const int lane = threadIdx.x;
   const int V = f.vehicles;
   if (b >= V) return;
