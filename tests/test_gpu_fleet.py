@@ -267,3 +267,24 @@ def test_fused_loop_falls_back_past_one_wave(cuda, golden):
         ft.close()
     for k in _LOOP_BUFFERS:
         np.testing.assert_array_equal(bufs[0][k], bufs[1][k], err_msg=k)
+
+
+def test_fused_loop_dispatch_order_past_the_wave_slots(cuda, golden):
+    """More vehicles than wave slots (2 per SIMD): the fused loop dispatches them longest reference
+    first (k_fleet_order); every vehicle still equals the stepped path bit for bit."""
+    import torch
+
+    props = torch.cuda.get_device_properties(0)
+    N, steps = 10, 25
+    V = 8 * props.multi_processor_count + 300
+    g, paths, starts, goals = _varied_fleet(golden, 13, seed=29)
+    idx = np.arange(V) % 13
+    bufs = []
+    for fused in (False, True):
+        ft = _tracker(N, V, 128, steps, fused=fused)
+        ft.reset_from_plans([paths[i] for i in idx], starts[idx], goals[idx])
+        ft.run()
+        bufs.append({k: ft.buffers()[k].cpu().numpy().copy() for k in _LOOP_BUFFERS})
+        ft.close()
+    for k in _LOOP_BUFFERS:
+        np.testing.assert_array_equal(bufs[0][k], bufs[1][k], err_msg=k)
