@@ -379,9 +379,14 @@ def config1_closed_loop() -> dict:
     planning = SimpleNamespace(plan=SimpleNamespace(success=True, path=path))
     maps = SimpleNamespace(start=tuple(plan["start"]), goal=tuple(plan["goal"]))
     tracker.track(planning, maps, map_resolution=0.8, visualize=False)  # warm (workspace, graph)
-    t0 = time.perf_counter()
-    states = tracker.track(planning, maps, map_resolution=0.8, visualize=False).states
-    gpu_s = time.perf_counter() - t0
+    # each leg is a ~5 ms host-driven loop: the best of three runs, so one scheduler stall or
+    # garbage collection does not set the number (the same rule for all three legs)
+    gpu_s = None
+    for _ in range(3):
+        t0 = time.perf_counter()
+        states = tracker.track(planning, maps, map_resolution=0.8, visualize=False).states
+        dt = time.perf_counter() - t0
+        gpu_s = dt if gpu_s is None else min(gpu_s, dt)
 
     # the same loop kept on the device: one vehicle of the fused fleet loop (mpcqp_fleet_loop, ONE
     # launch for the whole run: window, QP + relaxed retry, plant and goal test per step on the GPU)
@@ -391,7 +396,7 @@ def config1_closed_loop() -> dict:
     ft = FleetTracker(mpc, map_resolution=0.8, max_vehicles=1, max_ref_len=len(plan["path"]) * 8 + 64,
                       device="cuda:0", fused=True)
     loop_s = setup_s = None
-    for _ in range(3):  # warm, then the best of two
+    for _ in range(4):  # warm, then the best of three
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         ft.reset_from_plans([plan["path"]], np.asarray(plan["start"])[None], np.asarray(plan["goal"])[None])
@@ -415,9 +420,12 @@ def config1_closed_loop() -> dict:
             return None, None, None
         return o["u0"][0], o["X"][0], o["U"][0]
 
-    t0 = time.perf_counter()
-    c_states = mo.track_loop(params, ref_g, plan["start"], float(plan["yaw0"]), plan["goal"], 100, c_solve)
-    cpu_s = time.perf_counter() - t0
+    cpu_s = None
+    for _ in range(3):
+        t0 = time.perf_counter()
+        c_states = mo.track_loop(params, ref_g, plan["start"], float(plan["yaw0"]), plan["goal"], 100, c_solve)
+        dt = time.perf_counter() - t0
+        cpu_s = dt if cpu_s is None else min(cpu_s, dt)
     dev = max(float(np.abs(np.asarray(states) - np.asarray(c_states)).max()), 0.0) \
         if len(states) == len(c_states) else None
     return {
@@ -434,7 +442,8 @@ def config1_closed_loop() -> dict:
         "cpu_restatement_1core_s": cpu_s,
         "cpu_ms_per_step": 1e3 * cpu_s / max(1, len(c_states)),
         "max_state_diff_px": dev,
-        "note": "gpu_ms_per_step: the drop-in TrajectoryTracker loop, one B=1 launch + host sync per step; "
+        "note": "each leg the best of three runs after a warm one; "
+                "gpu_ms_per_step: the drop-in TrajectoryTracker loop, one B=1 launch + host sync per step; "
                 "gpu_device_loop_ms_per_step: the same loop as one vehicle of the fused device loop "
                 "(mpcqp_fleet_loop: one launch for the run, launch to results on the host; the "
                 "reference build and fleet buffer setup are gpu_device_loop_setup_s)",
