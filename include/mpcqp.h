@@ -382,7 +382,11 @@ int mpcqp_inflate(int B, int height, int width, int radius_px, const uint8_t* oc
 
 /* Workspace device buffers (for tests / inspection), layouts documented in DESIGN.md:
  *   model: K1 output, B x mpcqp_model_stride(N) doubles
- *   state: scaled QP + ADMM iterate (K2a/K2b output), B x mpcqp_state_stride(N) doubles */
+ *   state: scaled QP + ADMM iterate (K2a/K2b output), B x mpcqp_state_stride(N) doubles
+ * Both are allocated (max_batch QPs) at the first call that writes them: mpcqp_create for the
+ * long-horizon kernels, else an mpcqp_build with debug_state = 1 (model and state) or the stepped
+ * fleet (model).  The fused one-wave solve uses neither; NULL until then.  A first use inside a
+ * stream capture returns MPCQP_E_STATE (allocation cannot be captured): run it once uncaptured. */
 const double* mpcqp_model_buffer(const mpcqp_ws* ws);
 int mpcqp_model_stride(int horizon);
 const double* mpcqp_state_buffer(const mpcqp_ws* ws);

@@ -153,6 +153,25 @@ launcher_t launcher(const mpcqp_params& p) {
   if (wide_solve(p)) return p.reproducible == 0 && horizon <= MPCQP_MID_MAX_HORIZON ? &launch_mid : &launch_solve_wide;
   return horizon < MPCQP_WIDE_MIN_HORIZON ? kLaunchers[horizon] : nullptr;
 }
+int ensure_buffers(mpcqp_ws* ws, bool model, bool state, hipStream_t s) {
+  model = model && !ws->model;
+  state = state && !ws->state;
+  if (!model && !state) return MPCQP_OK;
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  if (s && hipStreamIsCapturing(s, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone)
+    return fail(MPCQP_E_STATE, "the workspace's model/state buffers are allocated at their first use, which "
+                               "cannot be inside a stream capture: run the call once uncaptured first");
+  int cur = -1;
+  hipError_t e = hipGetDevice(&cur);
+  if (e == hipSuccess && cur != ws->device) e = hipSetDevice(ws->device);
+  const int N = ws->p.horizon;
+  if (e == hipSuccess && model) e = hipMalloc(&ws->model, sizeof(double) * (size_t)model_stride(N) * (size_t)ws->max_batch);
+  if (e == hipSuccess && state)
+    e = hipMalloc(&ws->state, sizeof(double) * ws_state_stride(N, wide_solve(ws->p)) * (size_t)ws->max_batch);
+  if (cur >= 0 && cur != ws->device) (void)hipSetDevice(cur);
+  if (e != hipSuccess) return fail(MPCQP_E_HIP, std::string("hipMalloc (workspace buffers): ") + hipGetErrorString(e));
+  return MPCQP_OK;
+}
 fleet_loop_t fleet_looper(const mpcqp_params& p) {
   if (wide_solve(p) || p.debug_state || p.horizon < 1 || p.horizon >= MPCQP_WIDE_MIN_HORIZON) return nullptr;
   return kFleetLoops[p.horizon];
@@ -188,18 +207,17 @@ int mpcqp_create(const mpcqp_params* p, int max_batch, int device, mpcqp_ws** ws
   w->in_x0 = w->in_ref = w->in_up = nullptr;
   w->dparams = nullptr;
   w->dorder = nullptr;
-  const size_t mbytes = sizeof(double) * (size_t)model_stride(p->horizon) * (size_t)max_batch;
-  const size_t sbytes = sizeof(double) * ws_state_stride(p->horizon, mpcqp::wide_solve(*p)) * (size_t)max_batch;
-  e = hipMalloc(&w->model, mbytes);
-  if (e == hipSuccess) e = hipMalloc(&w->state, sbytes);
-  if (e == hipSuccess) e = hipMalloc(&w->dparams, 2 * sizeof(mpcqp_params));
+  e = hipMalloc(&w->dparams, 2 * sizeof(mpcqp_params));
   if (e == hipSuccess) e = hipMalloc(&w->dorder, sizeof(int32_t) * (size_t)max_batch);
   if (e != hipSuccess) {
-    if (w->model) (void)hipFree(w->model);
-    if (w->state) (void)hipFree(w->state);
     if (w->dparams) (void)hipFree(w->dparams);
     delete w;
     return fail(MPCQP_E_HIP, std::string("hipMalloc: ") + hipGetErrorString(e));
+  }
+  // the long-horizon kernels always read the model block and work in the state buffer
+  if (mpcqp::wide_solve(*p) && (rc = mpcqp::ensure_buffers(w, true, true, nullptr)) != MPCQP_OK) {
+    mpcqp_destroy(w);
+    return rc;
   }
   *ws = w;
   g_err.clear();
@@ -246,6 +264,11 @@ int mpcqp_build(mpcqp_ws* ws, int B, const double* x0, const double* ref, const 
     return MPCQP_OK;
   }
   hipStream_t s = static_cast<hipStream_t>(stream);
+  const int rc = mpcqp::ensure_buffers(ws, true, mpcqp::needs_state(ws->p), s);
+  if (rc) {
+    ws->built_B = -1;
+    return rc;
+  }
   hipLaunchKernelGGL(k_build, dim3(B), dim3(kWave), 0, s, ws->p, B, x0, ref, u_prev, ws->model);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return fail(MPCQP_E_HIP, std::string("k_build launch: ") + hipGetErrorString(e));

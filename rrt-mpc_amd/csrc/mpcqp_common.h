@@ -326,6 +326,9 @@ struct mpcqp_ws {
   int max_batch;
   int device;
   int built_B;
+  // per-QP model (K1 output) and solver state, allocated by ensure_buffers at the first call that
+  // needs them: the fused one-wave solve builds the model on chip and keeps the scaled problem
+  // there, so a workspace that only runs it holds neither (22 KB per QP at N = 20)
   double* model;
   double* state;
   // the inputs of the last mpcqp_build when the model is built inside the solve (fused K1)
@@ -345,4 +348,11 @@ namespace mpcqp {
 // false (nothing enqueued) when the parameter blocks do not run the one-wave kernel
 int enqueue_fleet_loop(mpcqp_ws* nominal, mpcqp_ws* relaxed, const mpcqp_fleet* f, int steps, const LoopTrigger& tr,
                        hipStream_t s, bool* fused);
+// allocate ws->model / ws->state (max_batch QPs) if requested and not yet there; refuses to allocate
+// on a capturing stream (the first use must run outside a capture); defined in mpcqp.hip
+int ensure_buffers(mpcqp_ws* ws, bool model, bool state, hipStream_t s);
+// the solver-state buffer is read or written: the long-horizon kernels' workspace, debug state
+inline bool needs_state(const mpcqp_params& p) { return wide_solve(p) || p.debug_state != 0; }
+// the stepped fleet's buffers (k_fleet_build writes the models; mpcqp_fleet.hip), before a capture
+int fleet_buffers(mpcqp_ws* nominal, mpcqp_ws* relaxed, hipStream_t s);
 }  // namespace mpcqp

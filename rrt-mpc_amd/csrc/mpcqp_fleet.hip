@@ -173,6 +173,8 @@ int enqueue_step(mpcqp_ws* nom, mpcqp_ws* rel, const mpcqp_fleet* f, hipStream_t
   const mpcqp::launcher_t solve = mpcqp::launcher(nom->p);
   if (mpcqp::launcher(rel->p) != solve) return fail(MPCQP_E_ARG, "nominal and relaxed workspaces differ in kernel");
   if (!solve) return fail(MPCQP_E_HORIZON, "horizon not compiled into this build");
+  const int rc = mpcqp::fleet_buffers(nom, rel, s);
+  if (rc) return rc;
   nom->built_B = -1;  // the fleet overwrites the models: a later mpcqp_solve needs its own build
   rel->built_B = -1;
   nom->in_x0 = nom->in_ref = nom->in_up = nullptr;
@@ -212,6 +214,10 @@ int run_graph(mpcqp_ws* nom, mpcqp_ws* rel, const mpcqp_fleet* f, int steps, hip
   if (e == hipSuccess) e = hipEventCreateWithFlags(&ev, hipEventDisableTiming);
   if (e == hipSuccess) e = hipEventRecord(ev, user);
   if (e == hipSuccess) e = hipStreamWaitEvent(s2, ev, 0);
+  if (e == hipSuccess && (rc = mpcqp::fleet_buffers(nom, rel, user)) != MPCQP_OK) {  // outside the capture
+    cleanup();
+    return rc;
+  }
   if (e == hipSuccess) e = hipStreamBeginCapture(s2, hipStreamCaptureModeThreadLocal);
   if (e != hipSuccess) {
     cleanup();
@@ -247,6 +253,12 @@ int mpcqp_fleet_step(mpcqp_ws* nominal, mpcqp_ws* relaxed, const mpcqp_fleet* f,
 }  // extern "C"
 
 namespace mpcqp {
+int fleet_buffers(mpcqp_ws* nominal, mpcqp_ws* relaxed, hipStream_t s) {
+  int rc = ensure_buffers(nominal, true, needs_state(nominal->p), s);
+  if (rc == MPCQP_OK) rc = ensure_buffers(relaxed, true, needs_state(relaxed->p), s);
+  return rc;
+}
+
 // the fused loop with the swarm's trigger (tr.max_replans > 0, mpcqp_swarm_loop) or without; nullptr
 // looper (mid / long horizons, reproducible or debug mode): *fused = false, nothing enqueued
 int enqueue_fleet_loop(mpcqp_ws* nominal, mpcqp_ws* relaxed, const mpcqp_fleet* f, int steps, const LoopTrigger& tr,

@@ -318,7 +318,8 @@ int mpcqp_swarm_run(mpcqp_ws* nominal, mpcqp_ws* relaxed, const mpcqp_fleet* f, 
   if (e == hipSuccess) e = hipEventCreateWithFlags(&ev, hipEventDisableTiming);
   if (e == hipSuccess) e = hipEventRecord(ev, user);
   if (e == hipSuccess) e = hipStreamWaitEvent(s2, ev, 0);
-  if (e == hipSuccess && (rc = set_replan_attrs(s)) != MPCQP_OK) {  // outside the capture
+  if (e == hipSuccess && ((rc = set_replan_attrs(s)) != MPCQP_OK ||  // outside the capture
+                          (rc = mpcqp::fleet_buffers(nominal, relaxed, user)) != MPCQP_OK)) {
     cleanup();
     return rc;
   }

@@ -47,10 +47,13 @@ def _solve_with_model(params, x0, ref, u_prev, **settings):
     torch.cuda.synchronize()
     out = {k: getattr(sol, k).cpu().numpy().copy() for k in sol._fields}
     L = _lib.lib()
-    model = np.zeros((B, L.mpcqp_model_stride(N)))
-    hip = ctypes.CDLL("libamdhip64.so")
-    hip.hipMemcpy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
-    assert hip.hipMemcpy(model.ctypes.data, L.mpcqp_model_buffer(ctrl._ws), model.nbytes, 2) == 0
+    ptr = L.mpcqp_model_buffer(ctrl._ws)
+    model = None  # the fused one-wave solve builds its model on chip: no model buffer
+    if ptr:
+        model = np.zeros((B, L.mpcqp_model_stride(N)))
+        hip = ctypes.CDLL("libamdhip64.so")
+        hip.hipMemcpy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
+        assert hip.hipMemcpy(model.ctypes.data, ptr, model.nbytes, 2) == 0
     ctrl.close()
     return out, model
 
