@@ -101,6 +101,8 @@ def test_iteration_indexing_bit_exact_on_product_path(cuda, cfg, N, B):
     {},                                       # the default polish schedule (early + near-tolerance)
     {"polish_near": 0.0},                     # early polish from iteration 150 only
     {"polish_from": 0, "polish_near": 0.0},   # OSQP's order: polish only after ADMM stops
+    {"polish_from": 25},                      # an attempt at every check (latency-bound loops)
+    {"polish_from": 50},
 ])
 def test_iteration_counts_match_cpu_restatement(cuda, schedule):
     """ADMM / polish iteration counts of the GPU against the C restatement (same algorithm),

@@ -35,17 +35,20 @@ def _default_plan(golden):
     return g, planning, maps
 
 
-@pytest.mark.parametrize("N,sim_steps", [(10, 100), (15, 300)])
-def test_tracker_reproduces_reference_closed_loop(cuda, golden, N, sim_steps):
+@pytest.mark.parametrize("N,sim_steps,settings", [(10, 100, {}), (15, 300, {}),
+                                                  (10, 100, {"polish_from": 25}), (15, 300, {"polish_from": 50})])
+def test_tracker_reproduces_reference_closed_loop(cuda, golden, N, sim_steps, settings):
     """BASELINE config 1 (N=10, 100 steps) and the code default (N=15): the reference's
     TrajectoryTracker loop (closed_loop.npz, exact solve substituted for OSQP) is reproduced
-    step for step with every QP solved on the GPU."""
+    step for step with every QP solved on the GPU -- also under the earlier polish schedules
+    measured for latency-bound loops, which reach the same exact optimum."""
     from mpcqp.config import MPCConfig, VizConfig
     from mpcqp.pipeline.control_stage import TrajectoryTracker
 
     g, planning, maps = _default_plan(golden)
     loop = golden("closed_loop.npz")
-    tracker = TrajectoryTracker(MPCConfig(horizon=N, sim_steps=sim_steps), VizConfig())
+    tracker = TrajectoryTracker(MPCConfig(horizon=N, sim_steps=sim_steps), VizConfig(),
+                                solver_settings=dict(settings), relaxed_solver_settings=dict(settings))
     result = tracker.track(planning, maps, map_resolution=float(g["map_resolution"]), visualize=False)
     states = np.asarray(result.states)
     ref_states = loop[f"N{N}_states"]
