@@ -31,16 +31,20 @@ SCHEDULES = [
 ]
 
 
+CASES = ["config1", "fleet100_N15"]
+
+
 def run(case, settings, dev):
     import torch
     from mpcqp import scenarios
     from mpcqp.config import MPCConfig
     from mpcqp.pipeline.fleet import FleetTracker
 
-    if case == "config1":
+    if case.startswith("config1"):  # config1 (N = 10) or config1_N<h>: the same vehicle at horizon h
         plan = scenarios.load_default_plan()
         paths, starts, goals = [plan["path"]], np.asarray(plan["start"])[None], np.asarray(plan["goal"])[None]
-        mpc, ref_len = MPCConfig(horizon=10, sim_steps=100), len(plan["path"]) * 8 + 64
+        h = int(case.split("_N")[1]) if "_N" in case else 10
+        mpc, ref_len = MPCConfig(horizon=h, sim_steps=300), len(plan["path"]) * 8 + 64
     else:
         paths, starts, goals = scenarios.fleet5(100)
         mpc, ref_len = MPCConfig(horizon=15, sim_steps=100), 160
@@ -65,11 +69,14 @@ def main() -> None:
     import torch
 
     dev = torch.device("cuda:0")
+    if len(sys.argv) > 1 and sys.argv[1] == "--single":  # one vehicle at several horizons
+        CASES[:] = ["config1_N10", "config1_N15", "config1_N20", "config1_N30"]
+        SCHEDULES[:] = [{}, {"polish_from": 25}, {"polish_from": 50}, {"polish_from": 75}]
     out = {"what": __doc__.split("\n\n")[0], "runs": []}
     base = {}
     for settings in SCHEDULES:
         row = {"settings": settings}
-        for case in ("config1", "fleet100_N15"):
+        for case in CASES:
             dt, states = run(case, settings, dev)
             if not settings:
                 base[case] = states
