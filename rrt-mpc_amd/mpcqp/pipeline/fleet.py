@@ -68,6 +68,17 @@ class FleetResult:
         return [TrackingResult(states=[s.copy() for s in st]) for st in self.states]
 
 
+def closed_loop_settings(horizon: int) -> dict:
+    """Polish schedule of the device closed loops (FleetTracker, Swarm).  A fleet's run is the sum
+    of each vehicle's step costs, so earlier polish attempts pay, where the library default
+    (`polish_from` 150) is tuned for a one-shot batch's slowest QP.  Measured with the fused loop at
+    N = 15 (profiles/r03_s12_schedule_fleets.json): `polish_from` 50 gives -4.8 / -5.4
+    / -5.6 % at 100 / 1024 / 4096 vehicles and -0.7 / -2.5 % on the config-5 swarm at 100 / 1024.
+    25, better for a lone vehicle at N <= 15, is slower for a fleet: its slowest vehicles' failed
+    attempts set the run.  Past the one-wave kernel the default stays (unmeasured)."""
+    return {"polish_from": 50} if horizon <= 31 else {}
+
+
 class FleetTracker:
     """V vehicles in closed loop on one GPU; every loop step runs on the device.
 
@@ -90,10 +101,14 @@ class FleetTracker:
         self.max_ref_len = int(max_ref_len)
         self.use_graph = bool(use_graph)
         self.fused = bool(fused)
+        # a closed loop pays every vehicle's step costs, not a batch's slowest QP: the polish schedule
+        # defaults to closed_loop_settings (the caller's settings win)
+        loop = closed_loop_settings(self.horizon)
+        settings = {**loop, **settings}
         self._nominal = BatchedMPCController(self.params, self.max_vehicles, device=device, **settings)
         # the retry's solver settings default to the nominal ones (control_stage.py:50-56 changes
         # only du_bounds and the reference speed)
-        rs = settings if relaxed_settings is None else relaxed_settings
+        rs = settings if relaxed_settings is None else {**loop, **relaxed_settings}
         self._relaxed = BatchedMPCController(relaxed_parameters(self.params), self.max_vehicles,
                                              device=self._nominal.device, **rs)
         self.device = self._nominal.device
@@ -253,4 +268,4 @@ class FleetTracker:
         self._relaxed.close()
 
 
-__all__ = ["FleetTracker", "FleetResult", "relaxed_parameters", "initial_state", "PHASE_NAMES"]
+__all__ = ["FleetTracker", "FleetResult", "relaxed_parameters", "initial_state", "closed_loop_settings", "PHASE_NAMES"]

@@ -58,7 +58,8 @@ class SwarmResult:
 class Swarm:
     def __init__(self, occupancy: np.ndarray, mpc, planner: PlannerParameters, *, map_resolution: float,
                  max_vehicles: int, max_ref_len: int = 512, device=None, replan_distance: float = 15.0,
-                 max_replans: int = 2, path_cap: int = 6144, use_graph: bool = True, fused: bool = False) -> None:
+                 max_replans: int = 2, path_cap: int = 6144, use_graph: bool = True, fused: bool = False,
+                 **settings) -> None:
         # path_cap: smoothed points a replan may produce.  The default is the most that the device
         # reference builder stages (kRefCap, csrc/mpcqp_swarm.hip), so a replanned path is never cut
         # shorter than a reference could be built from; capacity failures are reported apart from
@@ -66,8 +67,9 @@ class Swarm:
         self.occupancy = np.ascontiguousarray(occupancy, dtype=np.uint8)
         self.mpc = mpc
         self.planner = BatchedRRTStarPlanner(self.occupancy, planner, device=device)
+        # settings: solver settings of the vehicles' QPs (mpcqp_params names), as FleetTracker's
         self.fleet = FleetTracker(mpc, map_resolution=map_resolution, max_vehicles=max_vehicles,
-                                  max_ref_len=max_ref_len, device=self.planner.device)
+                                  max_ref_len=max_ref_len, device=self.planner.device, **settings)
         self.device = self.planner.device
         self.replan_distance = float(replan_distance)
         self.max_replans = int(max_replans)
