@@ -233,7 +233,7 @@ def host_threads() -> Tuple[int, int]:
     return threads, visible
 
 
-def spot_check(params, x0, ref, u_prev, U, active, status, idx, iters=None) -> dict:
+def spot_check(params, x0, ref, u_prev, U, active, status, idx, iters=None, settings=None) -> dict:
     """Checker: the GPU solutions of QPs `idx` against the C restatement, whose polish ends at the
     exact optimum of the QP (strictly convex: the same optimum OSQP+polish returns in the
     reference).  Parity against OSQP itself is unpinned here (OSQP is not installed)."""
@@ -242,7 +242,7 @@ def spot_check(params, x0, ref, u_prev, U, active, status, idx, iters=None) -> d
 
     idx = np.asarray(idx)
     threads, _ = host_threads()
-    out = cpu_solver.cpu_solve(params, x0[idx], ref[idx], u_prev[idx], nthreads=threads)
+    out = cpu_solver.cpu_solve(params, x0[idx], ref[idx], u_prev[idx], nthreads=threads, **(settings or {}))
     Uc = out["U"].reshape(len(idx), -1)
     Ug = np.asarray(U)[idx].reshape(len(idx), -1)
     err = np.abs(Ug - Uc).max(axis=1) / np.maximum(1.0, np.abs(Uc).max(axis=1))
@@ -266,16 +266,16 @@ def spot_check(params, x0, ref, u_prev, U, active, status, idx, iters=None) -> d
     return res
 
 
-def cpu_baseline(params, x0, ref, u_prev, seconds: float) -> dict:
+def cpu_baseline(params, x0, ref, u_prev, seconds: float, settings=None) -> dict:
     """The C restatement (oracle/, kind "port") on the host cores, bounded sample."""
     sys.path.insert(0, str(ROOT / "oracle"))
     import cpu_solver
 
     threads, visible = host_threads()
-    cpu_solver.cpu_solve(params, x0[:64], ref[:64], u_prev[:64], nthreads=threads)  # warm (build + page-in)
+    cpu_solver.cpu_solve(params, x0[:64], ref[:64], u_prev[:64], nthreads=threads, **(settings or {}))  # warm (build + page-in)
     done, solved, t0 = 0, 0, time.perf_counter()
     while True:
-        out = cpu_solver.cpu_solve(params, x0, ref, u_prev, nthreads=threads)
+        out = cpu_solver.cpu_solve(params, x0, ref, u_prev, nthreads=threads, **(settings or {}))
         done += len(x0)
         solved += int((out["status"] == 1).sum())
         if time.perf_counter() - t0 >= seconds:
@@ -284,7 +284,7 @@ def cpu_baseline(params, x0, ref, u_prev, seconds: float) -> dict:
     # the 1-core figure SURVEY.md 8(d) asks for beside the all-core one (a short slice)
     n1, t1 = 0, time.perf_counter()
     while time.perf_counter() - t1 < min(3.0, seconds / 3):
-        out1 = cpu_solver.cpu_solve(params, x0[:256], ref[:256], u_prev[:256], nthreads=1)
+        out1 = cpu_solver.cpu_solve(params, x0[:256], ref[:256], u_prev[:256], nthreads=1, **(settings or {}))
         n1 += int((out1["status"] == 1).sum())
     dt1 = time.perf_counter() - t1
     return {
@@ -563,7 +563,7 @@ def main() -> int:
 
     status = ctrl._status[:B].cpu().numpy()
     iters = ctrl._iters[:B].cpu().numpy()
-    flops = qp_flops(N, iters)
+    flops = qp_flops(N, iters, scaling=int(ctrl._cparams.scaling), check=int(ctrl._cparams.check_termination))
     T, (solved_all, flops_all, admm_all, pol_all) = reduce_stats(
         ctx, elapsed, [float((status == 1).sum()), float(flops.sum()), float(iters[:, 0].sum()),
                        float(iters[:, 1].sum())])
@@ -641,11 +641,11 @@ def main() -> int:
         if args.check_sample > 0:
             idx = np.unique(np.linspace(0, total - 1, min(total, args.check_sample)).astype(int))
             out["rel_err"] = spot_check(params, batch.x0, batch.ref, batch.u_prev, g["U"], g["active"],
-                                        g["status"], idx, g["iters"])
+                                        g["status"], idx, g["iters"], settings=extra)
             out["rel_err"]["gathered_qps"] = int(len(g["status"]))
             out["rel_err"]["gathered_solved"] = int((g["status"] == 1).sum())
         if world == 1 and args.cpu_seconds > 0:
-            out["cpu_baseline"] = cpu_baseline(params, x0, ref, u_prev, args.cpu_seconds)
+            out["cpu_baseline"] = cpu_baseline(params, x0, ref, u_prev, args.cpu_seconds, settings=extra)
         if world == 1 and not args.no_config1:
             out["config1"] = config1_closed_loop()
         if world == 1 and not args.no_config5 and args.config == "config3" and not args.horizon:

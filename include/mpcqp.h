@@ -94,13 +94,14 @@ typedef struct mpcqp_params {
   double adaptive_rho_tolerance; /* 5 (OSQP default) */
   int32_t max_iter;           /* 60000 */
   int32_t check_termination;  /* 25 (OSQP default) */
-  int32_t scaling;            /* 10 Ruiz iterations (OSQP default) */
+  int32_t scaling;            /* Ruiz iterations: 1 in this build's Python defaults (OSQP's default 10;
+                                 one pass halves the ADMM iterations on these QPs) */
   int32_t adaptive_rho;       /* 1 */
   int32_t adaptive_rho_interval; /* 25 (deterministic; OSQP's default is timing based) */
   int32_t polish;             /* 1 */
   int32_t polish_max_iter;    /* 100 */
   int32_t debug_state;        /* 1: also write the per-QP solver state buffer (mpcqp_state_buffer; tests) */
-  int32_t polish_from;        /* 150: from this ADMM iteration on, every termination check also tries the
+  int32_t polish_from;        /* 75 (Python default): from this ADMM iteration on, every termination check also tries the
                                  polish (capped at polish_attempt_max_iter); a polish that reaches a
                                  self-consistent active set is the exact optimum and ends the solve as
                                  solved, a failed attempt resumes ADMM.  0: polish only after ADMM stops */

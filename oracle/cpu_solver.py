@@ -72,10 +72,10 @@ def make_cparams(params, method: int = 0, **solver) -> CParams:
     c.slack_input = float(getattr(params, "slack_input", 5e2))
     c.slack_rate = float(getattr(params, "slack_rate", 5e2))
     settings = dict(rho=0.1, sigma=1e-6, alpha=1.6, eps_abs=1e-3, eps_rel=1e-3, adaptive_rho_tolerance=5.0,
-                    max_iter=60000, check_termination=25, scaling=10, adaptive_rho=1, adaptive_rho_interval=25,
-                    polish=1, polish_max_iter=100, polish_from=150, polish_attempt_max_iter=30,
+                    max_iter=60000, check_termination=25, scaling=1, adaptive_rho=1, adaptive_rho_interval=25,
+                    polish=1, polish_max_iter=100, polish_from=75, polish_attempt_max_iter=30,
                     polish_near=3.0)
-    settings.update(solver)
+    settings.update(solver)  # the defaults are the product's (mpcqp/_lib.py DEFAULT_SOLVER_SETTINGS)
     for k, v in settings.items():
         setattr(c, k, v)
     return c

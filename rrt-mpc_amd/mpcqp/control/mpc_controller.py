@@ -248,17 +248,14 @@ _CACHE_SIZE = 8
 
 def latency_settings(horizon: int) -> dict:
     """Polish schedule of the latency-bound B=1 drop-in (the reference's sequential loop, one QP
-    per call).  The library default (`polish_from` 150 with near-tolerance attempts) is tuned for a
-    batch, whose time is its slowest QP; one QP's own cost is lower with earlier attempts.
-    Measured on one vehicle's closed loop (profiles/r03_s10_schedule_single.json):
-    25 gives -18 % / -13 % at N = 10 / 15, 50 gives -5 % at N = 20 and -1.5 % at N = 30.  The
-    horizons past the one-wave kernel keep the default (unmeasured).  Every schedule ends at the
-    exact optimum; the counters match the C restatement under each (tests/test_gpu_parity.py)."""
-    if horizon <= 15:
-        return {"polish_from": 25}
-    if horizon <= 31:
-        return {"polish_from": 50}
-    return {}
+    per call).  The library default (`polish_from` 75 with near-tolerance attempts) is tuned for a
+    batch, whose time is its slowest QP; one QP's own cost is lower with an attempt at every
+    termination check.  Measured on one vehicle's closed loop with the default single Ruiz pass
+    (profiles/r03_s14_schedule_single.json): `polish_from` 25 is the fastest schedule
+    at N = 10, 15, 20 and 30.  The horizons past the one-wave kernel keep the default (unmeasured).
+    Every schedule ends at the exact optimum; the counters match the C restatement under each
+    (tests/test_gpu_parity.py)."""
+    return {"polish_from": 25} if horizon <= 31 else {}
 
 
 def _single_controller(params, method: str = "admm", **settings) -> BatchedMPCController:

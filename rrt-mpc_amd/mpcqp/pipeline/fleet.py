@@ -70,13 +70,13 @@ class FleetResult:
 
 def closed_loop_settings(horizon: int) -> dict:
     """Polish schedule of the device closed loops (FleetTracker, Swarm).  A fleet's run is the sum
-    of each vehicle's step costs, so earlier polish attempts pay, where the library default
-    (`polish_from` 150) is tuned for a one-shot batch's slowest QP.  Measured with the fused loop at
-    N = 15 (profiles/r03_s12_schedule_fleets.json): `polish_from` 50 gives -4.8 / -5.4
-    / -5.6 % at 100 / 1024 / 4096 vehicles and -0.7 / -2.5 % on the config-5 swarm at 100 / 1024.
-    25, better for a lone vehicle at N <= 15, is slower for a fleet: its slowest vehicles' failed
-    attempts set the run.  Past the one-wave kernel the default stays (unmeasured)."""
-    return {"polish_from": 50} if horizon <= 31 else {}
+    of each vehicle's step costs, so an attempt at every termination check pays, where the library
+    default (`polish_from` 75) is tuned for a one-shot batch's slowest QP.  Measured with the fused
+    loop at N = 15 and the default single Ruiz pass (DESIGN.md §9,
+    profiles/r03_s14_schedule_fleets.json): `polish_from` 25 against 75 gives -9 / -7 / -10 % at
+    100 / 1024 / 4096 vehicles and -5 % on the config-5 swarm.  Past the one-wave kernel the default
+    stays (unmeasured)."""
+    return {"polish_from": 25} if horizon <= 31 else {}
 
 
 class FleetTracker:

@@ -72,14 +72,15 @@ def main() -> None:
     if len(sys.argv) > 1 and sys.argv[1] == "--single":  # one vehicle at several horizons
         CASES[:] = ["config1_N10", "config1_N15", "config1_N20", "config1_N30"]
         SCHEDULES[:] = [{}, {"polish_from": 25}, {"polish_from": 50}, {"polish_from": 75}]
+        if len(sys.argv) > 2:  # --single '[{...}, ...]': these settings instead
+            SCHEDULES[:] = json.loads(sys.argv[2])
     out = {"what": __doc__.split("\n\n")[0], "runs": []}
     base = {}
     for settings in SCHEDULES:
         row = {"settings": settings}
         for case in CASES:
             dt, states = run(case, settings, dev)
-            if not settings:
-                base[case] = states
+            base.setdefault(case, states)  # differences against the first schedule
             diff = max(float(np.abs(a - b).max()) if a.shape == b.shape else float("inf")
                        for a, b in zip(states, base[case]))
             row[case] = {"seconds": dt, "steps": int(sum(len(s) for s in states)), "max_state_diff_px": diff}

@@ -1,7 +1,6 @@
 #!/usr/bin/env python3
 """Polish schedule on the fused fleets and swarm at scale: fused fleet loop (N = 15, 100 steps) at
-100 / 1024 / 4096 vehicles and the fused config-5 swarm at 100 / 1024 vehicles, the default schedule
-against polish_from 50, interleaved, best of three each.
+100 / 1024 / 4096 vehicles and the fused config-5 swarm at 100 / 1024 vehicles, polish_from 75 / 50 / 25, interleaved, best of three each.
 
     python tools/diag/schedule_fleets_large.py
 """
@@ -16,7 +15,7 @@ import numpy as np
 
 ROOT = Path(__file__).resolve().parents[2]
 sys.path[:0] = [str(ROOT / "rrt-mpc_amd"), str(ROOT / "tools")]
-SCHEDULES = [{}, {"polish_from": 50}]
+SCHEDULES = [{"polish_from": 75}, {"polish_from": 50}, {"polish_from": 25}]
 
 
 def fleet_time(V, settings, dev):
