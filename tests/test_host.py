@@ -96,6 +96,30 @@ def test_to_c_params_carries_reference_settings():
     assert (c.slack_velocity, c.slack_input, c.slack_rate) == (1e3, 5e2, 5e2)
 
 
+def test_checker_defaults_equal_product_defaults():
+    """The C restatement (oracle/cpu_solver.py) solves with the product's default settings, so a
+    default-settings comparison checks the same algorithm; and the per-workload schedules."""
+    import cpu_solver
+    from mpcqp._lib import DEFAULT_SOLVER_SETTINGS, to_c_params
+    from mpcqp.config import MPCConfig
+    from mpcqp.control.mpc_controller import latency_settings
+    from mpcqp.pipeline.fleet import closed_loop_settings
+
+    p = MPCConfig(horizon=20).to_parameters(0.8)
+    prod, chk = to_c_params(p), cpu_solver.make_cparams(p)
+    for name, _ in cpu_solver.CParams._fields_:
+        if name != "reproducible":  # the product's kernel choice; the C restatement has one algorithm
+            a, b = getattr(prod, name), getattr(chk, name)
+            a, b = (list(a), list(b)) if hasattr(a, "__len__") else (a, b)
+            assert a == b, name
+    # one Ruiz pass and the batch polish schedule (DESIGN.md §5); OSQP's 10 passes stay a setting
+    assert (DEFAULT_SOLVER_SETTINGS["scaling"], DEFAULT_SOLVER_SETTINGS["polish_from"]) == (1, 75)
+    assert to_c_params(p, scaling=10).scaling == 10
+    for N in (1, 10, 15, 20, 31):
+        assert latency_settings(N) == closed_loop_settings(N) == {"polish_from": 25}
+    assert latency_settings(40) == closed_loop_settings(40) == {}
+
+
 def test_config_defaults_mirror_reference():
     from mpcqp.config import MPCConfig
 
