@@ -98,11 +98,12 @@ def test_iteration_indexing_bit_exact_on_product_path(cuda, cfg, N, B):
 
 
 @pytest.mark.parametrize("schedule", [
-    {},                                       # the default polish schedule (early + near-tolerance)
-    {"polish_near": 0.0},                     # early polish from iteration 150 only
+    {},                                       # the default schedule (one Ruiz pass, early + near-tolerance polish)
+    {"polish_near": 0.0},                     # early polish from iteration polish_from (75) only
     {"polish_from": 0, "polish_near": 0.0},   # OSQP's order: polish only after ADMM stops
     {"polish_from": 25},                      # an attempt at every check (latency-bound loops)
     {"polish_from": 50},
+    {"scaling": 10, "polish_from": 150},      # OSQP's 10 Ruiz passes (the round-2 defaults)
 ])
 def test_iteration_counts_match_cpu_restatement(cuda, schedule):
     """ADMM / polish iteration counts of the GPU against the C restatement (same algorithm),
@@ -118,7 +119,7 @@ def test_iteration_counts_match_cpu_restatement(cuda, schedule):
     same = (out["iters"] == ref["iters"]).all(axis=1)
     # bit-exact iteration indexing on the product path: the wavefront tree reductions round
     # differently from the C code's sequential sums, but no counter decision flips on these QPs
-    # (profiles/r03_s4_iters_agreement.json: 100 % over 46k QPs of configs 2/3/4 and N = 1..31)
+    # (profiles/r03_s16_iters_agreement.json: 100 % over 52,224 QPs of configs 2/3/4 and N = 1..63)
     assert same.all(), f"QPs {np.flatnonzero(~same)[:10]} disagree on iteration counts"
     assert np.array_equal(out["status"], ref["status"])
     assert np.array_equal(out["active"], ref["active"])

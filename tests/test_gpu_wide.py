@@ -99,7 +99,7 @@ def test_long_horizons_bit_exact_with_c_restatement(cuda, N, settings):
 def test_long_horizons_fast_mode_against_c_restatement(cuda, N, settings):
     """The default (fast) long-horizon mode (the mid kernel): the same optimum, statuses, active sets
     and all four counters as the C restatement on every QP (its tree-order sums round differently,
-    but no counter decision flips: profiles/r03_s4_iters_agreement.json, 6 x 1024 QPs at N = 32..63)."""
+    but no counter decision flips: profiles/r03_s16_iters_agreement.json, 6 x 1024 QPs at N = 32..63)."""
     import cpu_solver
     from mpcqp import scenarios
 
