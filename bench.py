@@ -463,16 +463,136 @@ def config1_closed_loop() -> dict:
     }
 
 
-def load_pmc_traffic(N: int, batch: int):
-    """This workload's entry of the committed rocprofv3 PMC summary (HBM bytes, SQ counters), if present."""
+SOLVER_SETTING_FIELDS = ("method", "rho", "sigma", "alpha", "eps_abs", "eps_rel", "adaptive_rho_tolerance", "max_iter",
+                         "check_termination", "scaling", "adaptive_rho", "adaptive_rho_interval", "polish",
+                         "polish_max_iter", "polish_from", "polish_attempt_max_iter", "polish_near", "reproducible")
+
+
+def solver_settings(cparams) -> dict:
+    """The solver settings of an ``mpcqp_params`` block (the fields after MPCParameters')."""
+    return {k: getattr(cparams, k) for k in SOLVER_SETTING_FIELDS}
+
+
+def settings_key(cparams) -> str:
+    """Fingerprint of the solver settings a measurement ran with (keys the committed PMC passes)."""
+    import hashlib
+
+    return hashlib.sha256(json.dumps(solver_settings(cparams), sort_keys=True).encode()).hexdigest()[:16]
+
+
+def lib_key() -> str:
+    """Fingerprint of the kernel library the run loads (keys the committed PMC passes)."""
+    import hashlib
+
+    from mpcqp import _lib
+
+    h = hashlib.sha256()
+    with open(_lib.LIB_PATH, "rb") as f:
+        for chunk in iter(lambda: f.read(1 << 20), b""):
+            h.update(chunk)
+    return h.hexdigest()[:16]
+
+
+def method_label(cparams) -> str:
+    """What ran, against the reference's OSQP call (mpc_controller.py:119-132: rho 0.1, alpha 1.6,
+    eps 1e-3/1e-3, max_iter 60000, polish, adaptive_rho, OSQP defaults otherwise)."""
+    s = solver_settings(cparams)
+    if s["method"] != 0:
+        return "newton (semismooth-Newton polish only; not the reference's OSQP call)"
+    dev = []
+    if s["scaling"] != 10:
+        dev.append(f"scaling {s['scaling']} (OSQP default 10)")
+    if s["polish"] and (s["polish_from"] > 0 or s["polish_near"] > 0):
+        dev.append(f"early polish from ADMM iteration {s['polish_from']} / at {s['polish_near']:g}x the "
+                   f"tolerances, <= {s['polish_attempt_max_iter']} passes per attempt (OSQP: one polish after ADMM)")
+    dev.append(f"adaptive_rho_interval {s['adaptive_rho_interval']} (OSQP: timing-based)")
+    ref = dict(rho=0.1, alpha=1.6, eps_abs=1e-3, eps_rel=1e-3, max_iter=60000, polish=1, adaptive_rho=1, sigma=1e-6)
+    for k, v in ref.items():
+        if s[k] != v:
+            dev.append(f"{k} {s[k]:g} (reference {v:g})")
+    return ("admm+polish: OSQP's algorithm with the reference's settings (rho 0.1, alpha 1.6, eps 1e-3/1e-3, "
+            "max_iter 60000, polish, adaptive rho); deviations: " + "; ".join(dev))
+
+
+def load_pmc_traffic(N: int, batch: int, skey: str, lkey: str) -> Tuple[Optional[dict], Optional[str]]:
+    """This workload's entry of the committed rocprofv3 PMC summary (HBM bytes, SQ counters) when it
+    was measured with the same solver settings and the same kernel library; else (None, reason)."""
     p = ROOT / "profiles" / "pmc_traffic.json"
     if not p.exists():
-        return None
+        return None, "no committed PMC summary (profiles/pmc_traffic.json)"
     try:
-        d = json.loads(p.read_text())
-        return d.get(f"N{N}_B{batch}") or None
-    except Exception:
-        return None
+        e = json.loads(p.read_text()).get(f"N{N}_B{batch}")
+    except Exception as exc:  # pragma: no cover
+        return None, f"unreadable PMC summary: {exc}"
+    if not e:
+        return None, f"no PMC entry for N={N}, B={batch}"
+    if e.get("settings_key") != skey:
+        return None, f"PMC entry measured with other solver settings ({e.get('settings_key')} != {skey})"
+    if e.get("lib_key") != lkey:
+        return None, f"PMC entry measured with another kernel library ({e.get('lib_key')} != {lkey})"
+    return e, None
+
+
+OSQP_SETTINGS = {"scaling": 10, "polish_from": 0, "polish_near": 0.0}
+
+
+def osqp_settings_leg(params, x0, ref, u_prev, steps: int, warmup: int, device, method: str, extra: dict,
+                      check: int) -> dict:
+    """The same batch with OSQP's own defaults where this build's differ (10 Ruiz passes, one polish
+    after ADMM stops; mpc_controller.py:119-132 sets nothing else), timed like the headline leg
+    (events on the launch stream around each step's solve launch), spot-checked the same way."""
+    import torch
+
+    from mpcqp import _lib
+    from mpcqp.control.mpc_controller import BatchedMPCController
+
+    B, N = len(x0), int(params.horizon)
+    sett = {**extra, **OSQP_SETTINGS}
+    ctrl = BatchedMPCController(params, max(1, B), device=device, method=method, **sett)
+    try:
+        x0_t, ref_t, up_t = (torch.from_numpy(a).to(device) for a in (x0, ref, u_prev))
+        L = _lib.lib()
+        stream = torch.cuda.current_stream(device)
+        s = ctypes.c_void_p(stream.cuda_stream)
+        ev = [[torch.cuda.Event(enable_timing=True) for _ in range(2)] for _ in range(steps)]
+
+        def step(k: int) -> None:
+            if k >= 0:
+                ev[k][0].record(stream)
+            _lib.check(L.mpcqp_build(ctrl._ws, B, x0_t.data_ptr(), ref_t.data_ptr(), up_t.data_ptr(), s), "build")
+            _lib.check(L.mpcqp_solve(ctrl._ws, B, ctrl._u0.data_ptr(), ctrl._X.data_ptr(), ctrl._U.data_ptr(),
+                                     ctrl._status.data_ptr(), ctrl._iters.data_ptr(), ctrl._active.data_ptr(), s),
+                       "solve")
+            if k >= 0:
+                ev[k][1].record(stream)
+
+        elapsed = timed_steps(step, steps, warmup, DistContext(), lambda: torch.cuda.synchronize(device))
+        k2_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in ev]))
+        status = ctrl._status[:B].cpu().numpy()
+        iters = ctrl._iters[:B].cpu().numpy()
+        flops = qp_flops(N, iters, scaling=int(ctrl._cparams.scaling), check=int(ctrl._cparams.check_termination))
+        tf = float(flops.sum()) / (k2_ms * 1e-3) / 1e12
+        out = {
+            "value": float((status == 1).sum()) * steps / elapsed,
+            "unit": "QP/s",
+            "ms_per_step": 1e3 * elapsed / steps,
+            "k_solve_ms": k2_ms,
+            "method": method_label(ctrl._cparams),
+            "solver_settings": solver_settings(ctrl._cparams),
+            "solved_fraction": float((status == 1).mean()),
+            "iters_mean": {"admm": float(iters[:, 0].mean()), "polish": float(iters[:, 1].mean())},
+            "roofline": {"bound": "fp64_valu", "achieved": tf, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
+                         "frac": tf / FP64_PEAK_TFLOPS},
+            "note": "the headline batch under OSQP's defaults where this build's defaults differ (scaling 10, "
+                    "polish once after ADMM); same timing rule as the headline line",
+        }
+        if check > 0:
+            idx = np.unique(np.linspace(0, B - 1, min(B, check)).astype(int))
+            out["rel_err"] = spot_check(params, x0, ref, u_prev, ctrl._U[:B].cpu().numpy(),
+                                        ctrl._active[:B].cpu().numpy(), status, idx, iters, settings=sett)
+        return out
+    finally:
+        ctrl.close()
 
 
 # ------------------------------------------------------------------ main
@@ -497,6 +617,8 @@ def main() -> int:
     ap.add_argument("--check-sample", type=int, default=512, help="QPs of the gathered result rank 0 checks")
     ap.add_argument("--no-config1", action="store_true", help="skip the config-1 closed-loop line")
     ap.add_argument("--no-config5", action="store_true", help="skip the config-5 swarm line")
+    ap.add_argument("--no-osqp-settings", action="store_true",
+                    help="skip the leg that reruns the batch under OSQP's own scaling / polish defaults")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="torch.distributed backend for N > 1 (nccl = RCCL; gloo only to rehearse "
                          "several ranks on one GPU)")
@@ -578,7 +700,9 @@ def main() -> int:
         ms_per_step = 1000.0 * T / args.steps
         achieved_tf = float(flops.sum()) / (k2_ms * 1e-3) / 1e12  # rank-0 K2 launch, algorithmic flops
         hbm_gbs = total * qp_bytes(N) / (ms_per_step * 1e-3) / 1e9
-        pmc = load_pmc_traffic(N, B) or {}
+        skey, lkey = settings_key(ctrl._cparams), lib_key()
+        pmc, pmc_reason = load_pmc_traffic(N, B, skey, lkey)
+        pmc = pmc or {}
         traffic = pmc.get("k_solve_hbm_bytes_per_launch")
         hw_flops = (pmc.get("k_solve_sq") or {}).get("hw_fp64_flops_per_launch")
         metric = BASELINE_METRIC if (args.config, N, per_gpu, strong) == ("config3", 20, 4096, False) else \
@@ -605,8 +729,8 @@ def main() -> int:
                 "horizon": N,
                 "nx": 4,
                 "nu": 2,
-                "method": "admm+polish (OSQP algorithm, reference settings)" if args.method == "admm"
-                else "newton (polish only)",
+                "method": method_label(ctrl._cparams),
+                "solver_settings": solver_settings(ctrl._cparams),
                 "parallelism": f"dp{world} (independent contiguous shards, {'strong' if strong else 'weak'})",
             },
             "solved_fraction": solved_all / total,
@@ -623,6 +747,9 @@ def main() -> int:
                 # the hardware's own count (SQ_INSTS_VALU_FLOPS_FP64, committed PMC pass) over this launch time
                 "hw_flops_per_launch": hw_flops,
                 "hw_frac": hw_flops / (k2_ms * 1e-3) / 1e12 / FP64_PEAK_TFLOPS if hw_flops else None,
+                # the PMC entry counts only when measured with these settings and this library
+                "pmc_key": {"settings": skey, "lib": lkey},
+                "pmc_null_reason": pmc_reason,
                 "note": "FP64 VALU roof (MI355X FP64 vector peak 78.6 TF; no MFMA is issued: f64 MFMA has "
                         "the same peak and the per-QP matrices are <= 62x62). k_solve is a latency-bound "
                         "FP64 VALU kernel. Flops = bench.qp_flops (as implemented, counted per QP from the "
@@ -644,6 +771,9 @@ def main() -> int:
                                         g["status"], idx, g["iters"], settings=extra)
             out["rel_err"]["gathered_qps"] = int(len(g["status"]))
             out["rel_err"]["gathered_solved"] = int((g["status"] == 1).sum())
+        if world == 1 and not args.no_osqp_settings:
+            out["osqp_settings"] = osqp_settings_leg(params, x0, ref, u_prev, args.steps, args.warmup, device,
+                                                     args.method, extra, min(args.check_sample, 256))
         if world == 1 and args.cpu_seconds > 0:
             out["cpu_baseline"] = cpu_baseline(params, x0, ref, u_prev, args.cpu_seconds, settings=extra)
         if world == 1 and not args.no_config1:

@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define MPCQP_ABI_VERSION 6
+#define MPCQP_ABI_VERSION 7
 
 /* error codes (function return values) */
 #define MPCQP_OK 0
@@ -44,6 +44,8 @@ extern "C" {
 #define MPCQP_E_BATCH (-3)       /* B > max_batch of the workspace */
 #define MPCQP_E_HIP (-4)         /* HIP runtime / launch error */
 #define MPCQP_E_STATE (-5)       /* mpcqp_solve before mpcqp_build of the same B */
+#define MPCQP_E_DEVICE (-6)      /* the device reported a fault at a stream synchronisation (sticky:
+                                    an earlier kernel faulted; the device context is unusable) */
 
 #define MPCQP_MAX_HORIZON 1024   /* per-QP workspace 16 (2N)^2 bytes: 67 MB at N = 1024 */
 #define MPCQP_WIDE_MIN_HORIZON 32 /* N <= 31: one wave per QP (2N variables on the lanes, the KKT
@@ -52,9 +54,17 @@ extern "C" {
                                      rows split in four column parts over their registers; beyond, and in
                                      reproducible mode, 256 threads restating the C code */
 
-/* per-QP status codes (mirror OSQP's; mpc_controller.py:137 accepts 1 and 2) */
+/* per-QP status codes (mirror OSQP's; mpc_controller.py:137 accepts 1 and 2).
+ * Where the meaning differs from OSQP's: OSQP reports "solved" whenever ADMM met eps_abs/eps_rel and
+ * records a failed polish separately (info.status_polish = -1, the ADMM iterate returned).  This
+ * library reports that case as MPCQP_SOLVED_INACCURATE (2), the ADMM iterate returned as OSQP does,
+ * so MPCQP_SOLVED (1) always means the polished exact optimum.  The reference accepts both codes
+ * (mpc_controller.py:137), so its loop behaves the same; a batch consumer counting OSQP "solved"
+ * should count 1 and 2 when ADMM converged (iters[1] > 0 marks that a polish ran). */
 #define MPCQP_SOLVED 1            /* polish converged: exact optimum (active set reproduces itself) */
-#define MPCQP_SOLVED_INACCURATE 2 /* ADMM met eps_abs/eps_rel but polish did not converge */
+#define MPCQP_SOLVED_INACCURATE 2 /* ADMM met eps_abs/eps_rel but polish did not converge (OSQP: solved,
+                                     status_polish -1), or max_iter reached within 10x the tolerances
+                                     (OSQP: solved_inaccurate) */
 #define MPCQP_MAX_ITER_REACHED (-2)
 #define MPCQP_NUMERICAL_ERROR (-10) /* non-finite data or non-positive pivot */
 
@@ -167,6 +177,21 @@ int mpcqp_build(mpcqp_ws* ws, int B, const double* x0, const double* ref, const 
  */
 int mpcqp_solve(mpcqp_ws* ws, int B, double* u0, double* X, double* U, int32_t* status,
                 int32_t* iters, uint8_t* active, void* stream);
+
+/*
+ * B = 1 low-latency path (ABI 7): the sequential closed loop of TrajectoryTracker.track solves one QP
+ * per step (control_stage.py:100-129), where host overhead, not the kernel, decides the step time.
+ * The workspace owns two blocks of pinned, device-mapped, coherent host memory and a private
+ * non-blocking stream, allocated by the first mpcqp_stage:
+ *   in   doubles: x0[4] | ref[(N+1) x 4] | u_prev[2]          (the caller writes them in place)
+ *   out  bytes at offsets[0..5]: u0 (2 f64) | X (4 x (N+1) f64) | U (2 x N f64) | status (i32) |
+ *        iters (4 i32) | active (5N+1 u8)                     (the kernels write them in place)
+ * mpcqp_solve_staged runs mpcqp_build + mpcqp_solve for the one QP in the `in` block on that stream
+ * and waits for it: one launch, no copy commands, one synchronisation.  The outputs are then in the
+ * `out` block.  MPCQP_E_DEVICE when a fault surfaces at the synchronisation.
+ * Replaces the per-call cvxpy build + OSQP solve of MPCController.solve (mpc_controller.py:53-141). */
+int mpcqp_stage(mpcqp_ws* ws, double** in, void** out, int32_t offsets[6]);
+int mpcqp_solve_staged(mpcqp_ws* ws);
 
 /*
  * Closed-loop fleet: V vehicles tracking their own references, one MPC step each per call

@@ -207,6 +207,9 @@ int mpcqp_create(const mpcqp_params* p, int max_batch, int device, mpcqp_ws** ws
   w->in_x0 = w->in_ref = w->in_up = nullptr;
   w->dparams = nullptr;
   w->dorder = nullptr;
+  w->stage_in = w->stage_in_d = nullptr;
+  w->stage_out = w->stage_out_d = nullptr;
+  w->stage_stream = nullptr;
   e = hipMalloc(&w->dparams, 2 * sizeof(mpcqp_params));
   if (e == hipSuccess) e = hipMalloc(&w->dorder, sizeof(int32_t) * (size_t)max_batch);
   if (e != hipSuccess) {
@@ -246,6 +249,10 @@ void mpcqp_destroy(mpcqp_ws* ws) {
   (void)hipFree(ws->state);
   (void)hipFree(ws->dparams);
   (void)hipFree(ws->dorder);
+  if (ws->stage_stream) (void)hipStreamSynchronize(ws->stage_stream);
+  if (ws->stage_in) (void)hipHostFree(ws->stage_in);
+  if (ws->stage_out) (void)hipHostFree(ws->stage_out);
+  if (ws->stage_stream) (void)hipStreamDestroy(ws->stage_stream);
   delete ws;
 }
 
@@ -288,6 +295,79 @@ int mpcqp_solve(mpcqp_ws* ws, int B, double* u0, double* X, double* U, int32_t* 
   mpcqp::launcher(ws->p)(s, L);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return fail(MPCQP_E_HIP, std::string("k_solve launch: ") + hipGetErrorString(e));
+  return MPCQP_OK;
+}
+
+// ------------------------------------------------------------------ B = 1 path
+// Output block layout of the staged path (include/mpcqp.h): u0 | X | U | status | iters | active.
+static void stage_offsets(int N, int32_t off[7]) {
+  off[0] = 0;                        // u0     2 f64
+  off[1] = 16;                       // X      4 x (N+1) f64
+  off[2] = off[1] + 32 * (N + 1);    // U      2 x N f64
+  off[3] = off[2] + 16 * N;          // status i32
+  off[4] = off[3] + 4;               // iters  4 x i32
+  off[5] = off[4] + 16;              // active 5N+1 u8
+  off[6] = off[5] + 5 * N + 1;       // total bytes
+}
+
+int mpcqp_stage(mpcqp_ws* ws, double** in, void** out, int32_t offsets[6]) {
+  if (!ws) return fail(MPCQP_E_ARG, "null ws");
+  const int N = ws->p.horizon;
+  int32_t off[7];
+  stage_offsets(N, off);
+  if (!ws->stage_in) {
+    int cur = -1;
+    hipError_t e = hipGetDevice(&cur);
+    if (e == hipSuccess && cur != ws->device) e = hipSetDevice(ws->device);
+    const unsigned fl = hipHostMallocMapped | hipHostMallocCoherent;
+    double* hin = nullptr;
+    uint8_t* hout = nullptr;
+    void* din = nullptr;
+    void* dout = nullptr;
+    hipStream_t st = nullptr;
+    if (e == hipSuccess) e = hipHostMalloc((void**)&hin, sizeof(double) * (size_t)(4 * (N + 1) + 6), fl);
+    if (e == hipSuccess) e = hipHostMalloc((void**)&hout, (size_t)off[6], fl);
+    if (e == hipSuccess) e = hipHostGetDevicePointer(&din, hin, 0);
+    if (e == hipSuccess) e = hipHostGetDevicePointer(&dout, hout, 0);
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&st, hipStreamNonBlocking);
+    if (cur >= 0 && cur != ws->device) (void)hipSetDevice(cur);
+    if (e != hipSuccess) {
+      if (hin) (void)hipHostFree(hin);
+      if (hout) (void)hipHostFree(hout);
+      return fail(MPCQP_E_HIP, std::string("B=1 staging blocks: ") + hipGetErrorString(e));
+    }
+    std::memset(hin, 0, sizeof(double) * (size_t)(4 * (N + 1) + 6));
+    std::memset(hout, 0, (size_t)off[6]);
+    ws->stage_in = hin;
+    ws->stage_in_d = static_cast<double*>(din);
+    ws->stage_out = hout;
+    ws->stage_out_d = static_cast<uint8_t*>(dout);
+    ws->stage_stream = st;
+  }
+  if (in) *in = ws->stage_in;
+  if (out) *out = ws->stage_out;
+  if (offsets)
+    for (int i = 0; i < 6; ++i) offsets[i] = off[i];
+  return MPCQP_OK;
+}
+
+int mpcqp_solve_staged(mpcqp_ws* ws) {
+  if (!ws) return fail(MPCQP_E_ARG, "null ws");
+  if (!ws->stage_in) return fail(MPCQP_E_STATE, "mpcqp_solve_staged before mpcqp_stage");
+  const int N = ws->p.horizon;
+  int32_t off[7];
+  stage_offsets(N, off);
+  const double* d = ws->stage_in_d;
+  uint8_t* o = ws->stage_out_d;
+  hipStream_t s = ws->stage_stream;
+  int rc = mpcqp_build(ws, 1, d, d + 4, d + 4 + 4 * (N + 1), s);
+  if (rc) return rc;
+  rc = mpcqp_solve(ws, 1, reinterpret_cast<double*>(o + off[0]), reinterpret_cast<double*>(o + off[1]),
+                   reinterpret_cast<double*>(o + off[2]), reinterpret_cast<int32_t*>(o + off[3]),
+                   reinterpret_cast<int32_t*>(o + off[4]), o + off[5], s);
+  if (rc) return rc;
+  const hipError_t e = hipStreamSynchronize(s);
+  if (e != hipSuccess) return fail(MPCQP_E_DEVICE, std::string("hipStreamSynchronize: ") + hipGetErrorString(e));
   return MPCQP_OK;
 }
 

@@ -341,6 +341,12 @@ struct mpcqp_ws {
   mpcqp_params* dparams;
   // the fused loop's dispatch order (max_batch vehicles), written by k_fleet_order on the stream
   int32_t* dorder;
+  // the B = 1 path (mpcqp_stage / mpcqp_solve_staged): mapped host blocks and a private stream
+  double* stage_in;      // host address (x0 | ref | u_prev)
+  double* stage_in_d;    // its device address
+  uint8_t* stage_out;    // host address (u0 | X | U | status | iters | active)
+  uint8_t* stage_out_d;  // its device address
+  hipStream_t stage_stream;
 };
 
 namespace mpcqp {

@@ -34,7 +34,8 @@ STATUS_NAMES = {
 
 # OSQP settings used by the reference (src/control/mpc_controller.py:121-131) plus the
 # OSQP defaults it relies on implicitly.
-ABI_VERSION = 6  # MPCQP_ABI_VERSION (include/mpcqp.h)
+ABI_VERSION = 7  # MPCQP_ABI_VERSION (include/mpcqp.h)
+E_DEVICE = -6  # MPCQP_E_DEVICE: a fault surfaced at a stream synchronisation
 
 DEFAULT_SOLVER_SETTINGS = dict(
     rho=0.1,
@@ -213,7 +214,13 @@ class MpcqpSwarm(ctypes.Structure):
 
 
 class LibraryError(RuntimeError):
-    pass
+    """A library call refused its arguments or failed to launch (mpcqp_* return code)."""
+
+
+class DeviceError(RuntimeError):
+    """The HIP runtime reported a failure outside a launch: an allocation, or a stream sync at which
+    an earlier kernel's fault surfaced (sticky: the device context is unusable afterwards).  Not a
+    LibraryError, so the drop-in's map-a-failed-solve-to-None path never swallows it."""
 
 
 _lib: Optional[ctypes.CDLL] = None
@@ -259,6 +266,9 @@ _SYMBOLS = {
     "mpcqp_ws_state_stride": ([ctypes.c_void_p], ctypes.c_int),
     "mpcqp_debug_wave_ops": ([ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p], ctypes.c_int),
     "mpcqp_debug_stamps": ([ctypes.c_void_p, ctypes.c_int], ctypes.c_int),
+    "mpcqp_stage": ([ctypes.c_void_p, ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_void_p),
+                     ctypes.POINTER(ctypes.c_int32)], ctypes.c_int),
+    "mpcqp_solve_staged": ([ctypes.c_void_p], ctypes.c_int),
 }
 
 
@@ -291,59 +301,6 @@ def lib() -> ctypes.CDLL:
     return handle
 
 
-_hip: Optional[ctypes.CDLL] = None
-
-
-def hip() -> ctypes.CDLL:
-    """The HIP runtime (loaded by torch and libmpcqp.so already): mapped host memory and stream
-    syncs for the B=1 path."""
-    global _hip
-    if _hip is None:
-        h = ctypes.CDLL("libamdhip64.so")
-        h.hipHostMalloc.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_size_t, ctypes.c_uint]
-        h.hipHostMalloc.restype = ctypes.c_int
-        h.hipHostGetDevicePointer.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_void_p, ctypes.c_uint]
-        h.hipHostGetDevicePointer.restype = ctypes.c_int
-        h.hipHostFree.argtypes = [ctypes.c_void_p]
-        h.hipHostFree.restype = ctypes.c_int
-        h.hipStreamSynchronize.argtypes = [ctypes.c_void_p]
-        h.hipStreamSynchronize.restype = ctypes.c_int
-        _hip = h
-    return _hip
-
-
-HIP_HOST_MALLOC_MAPPED = 0x2
-HIP_HOST_MALLOC_COHERENT = 0x40000000
-
-
-class MappedHostBuffer:
-    """Pinned, device-mapped, coherent host memory (hipHostMalloc): the kernels read and write it
-    in place, so a B=1 solve needs no copy commands -- one launch and one stream sync."""
-
-    def __init__(self, nbytes: int) -> None:
-        h = hip()
-        self.host = ctypes.c_void_p()
-        self.dev = ctypes.c_void_p()
-        self.nbytes = int(nbytes)
-        err = h.hipHostMalloc(ctypes.byref(self.host), self.nbytes, HIP_HOST_MALLOC_MAPPED | HIP_HOST_MALLOC_COHERENT)
-        if err != 0 or not self.host.value:
-            raise LibraryError(f"hipHostMalloc failed: hipError_t {err}")
-        err = h.hipHostGetDevicePointer(ctypes.byref(self.dev), self.host, 0)
-        if err != 0 or not self.dev.value:
-            h.hipHostFree(self.host)
-            self.host = ctypes.c_void_p()
-            raise LibraryError(f"hipHostGetDevicePointer failed: hipError_t {err}")
-
-    def array(self, dtype, count: int, offset: int = 0) -> np.ndarray:
-        buf = (ctypes.c_uint8 * self.nbytes).from_address(self.host.value)
-        return np.frombuffer(buf, dtype=dtype, count=count, offset=offset)
-
-    def free(self) -> None:
-        if self.host.value:
-            hip().hipHostFree(self.host)
-            self.host = ctypes.c_void_p()
-
-
 def check(rc: int, what: str) -> None:
     if rc != 0:
         msg = lib().mpcqp_last_error().decode(errors="replace")
@@ -369,6 +326,7 @@ __all__ = [
     "lib",
     "check",
     "LibraryError",
+    "DeviceError",
     "DEFAULT_SOLVER_SETTINGS",
     "STATUS_NAMES",
     "SOLVED",

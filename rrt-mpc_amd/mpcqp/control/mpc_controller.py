@@ -12,7 +12,6 @@ from __future__ import annotations
 
 import ctypes
 import logging
-import os
 from collections import OrderedDict
 from dataclasses import dataclass
 from typing import NamedTuple, Optional, Tuple
@@ -56,20 +55,33 @@ class BatchSolution(NamedTuple):
     active: "object"  # (B, 5N+1) uint8 {0 inactive, 1 lower, 2 upper} per soft row
 
 
+def _arr_key(a) -> bytes:
+    if type(a) is np.ndarray and a.dtype == np.float64 and a.flags.c_contiguous:
+        return a.tobytes()
+    return np.asarray(a, float).tobytes()
+
+
+def _tuple_key(a):
+    return a if type(a) is tuple else np.asarray(a, float).tobytes()
+
+
 def _params_key(params, method: int, settings: dict) -> tuple:
+    """Value key of a parameter block + solver settings (the B=1 controller cache; computed once per
+    drop-in solve, so it avoids array conversions where the fields already are float64 arrays /
+    tuples, as MPCConfig.to_parameters and dataclasses.replace produce them)."""
     return (
-        int(params.horizon),
-        float(params.wheelbase_px),
-        float(params.dt),
-        np.asarray(params.q, float).tobytes(),
-        np.asarray(params.r, float).tobytes(),
-        np.asarray(params.q_terminal, float).tobytes(),
-        np.asarray(params.u_bounds, float).tobytes(),
-        np.asarray(params.v_bounds, float).tobytes(),
-        np.asarray(params.du_bounds, float).tobytes(),
-        float(getattr(params, "slack_velocity", 1e3)),
-        float(getattr(params, "slack_input", 5e2)),
-        float(getattr(params, "slack_rate", 5e2)),
+        params.horizon,
+        params.wheelbase_px,
+        params.dt,
+        _arr_key(params.q),
+        _arr_key(params.r),
+        _arr_key(params.q_terminal),
+        _tuple_key(params.u_bounds),
+        _tuple_key(params.v_bounds),
+        _tuple_key(params.du_bounds),
+        getattr(params, "slack_velocity", 1e3),
+        getattr(params, "slack_input", 5e2),
+        getattr(params, "slack_rate", 5e2),
         int(method),
         tuple(sorted(settings.items())),
     )
@@ -160,77 +172,64 @@ class BatchedMPCController:
                              self._active[:B])
 
     def solve_one(self, x0, ref, u_prev=None):
-        """One QP for the sequential closed loop of ``TrajectoryTracker.track``, where the copies
-        dominate a B=1 step.  Inputs and outputs are packed into one block each of pinned,
-        device-mapped host memory that the kernels read and write in place: no copy commands,
-        one stream sync.  (``MPCQP_B1_STAGING=copy`` stages through device buffers instead: one
-        host->device and one device->host copy.)  ``x0`` (4,), ``ref`` (N+1, 4), ``u_prev`` (2,)
-        host arrays.  Returns host numpy ``(status, u0, X, U)``; X (4, N+1) and U (2, N) are fresh
-        arrays."""
-        torch = self._torch
-        N = self.horizon
-        io = getattr(self, "_one", None)
+        """One QP for the sequential closed loop of ``TrajectoryTracker.track``, where host overhead
+        dominates a B=1 step.  The workspace's own blocks of pinned, device-mapped host memory hold
+        the inputs and outputs, which the kernels read and write in place (``mpcqp_stage`` /
+        ``mpcqp_solve_staged``, include/mpcqp.h): the inputs are written into the block, then ONE
+        library call launches the solve on the workspace's private stream and waits for it.
+        ``x0`` (4,), ``ref`` (>= N+1, 4) -- rows 0..N are used --, ``u_prev`` (2,) host arrays.
+        Returns host numpy ``(status, u0, X, U)``; X (4, N+1) and U (2, N) are fresh arrays.
+        A fault that surfaces at the synchronisation raises ``_lib.DeviceError``."""
+        io = self._one
         if io is None:
-            io = self._one = self._one_buffers()
-        h = io["hin_np"]
-        h[0:4] = np.asarray(x0, dtype=np.float64).reshape(4)
-        h[4:4 + 4 * (N + 1)] = np.asarray(ref, dtype=np.float64).reshape(-1)[: 4 * (N + 1)]
-        h[4 + 4 * (N + 1):] = 0.0 if u_prev is None else np.asarray(u_prev, dtype=np.float64).reshape(2)
-        stream = torch.cuda.current_stream(self.device)
-        s = ctypes.c_void_p(stream.cuda_stream)
-        o = io["offs"]
-        if io["mapped"]:
-            d, b = io["din_ptr"], io["dout_ptr"]
+            io = self._one = self._stage()
+        io["x0"][:] = x0
+        io["ref"][:] = ref[: self.horizon + 1]
+        if u_prev is None:
+            io["up"][:] = 0.0
         else:
-            io["din"].copy_(io["hin"], non_blocking=True)
-            d, b = io["din"].data_ptr(), io["dout"].data_ptr()
-        _lib.check(self._L.mpcqp_build(self._ws, 1, d, d + 32, d + 32 * (N + 2), s), "mpcqp_build")
-        _lib.check(self._L.mpcqp_solve(self._ws, 1, b + o["u0"], b + o["X"], b + o["U"], b + o["status"],
-                                       b + o["iters"], b + o["active"], s), "mpcqp_solve")
-        if io["mapped"]:
-            _lib.check(_lib.hip().hipStreamSynchronize(s), "hipStreamSynchronize")
-        else:
-            io["hout"].copy_(io["dout"], non_blocking=True)
-            stream.synchronize()
-        hb = io["hout_np"]
-        status = int(np.frombuffer(hb, np.int32, 1, o["status"])[0])
-        u0 = np.frombuffer(hb, np.float64, 2, o["u0"]).copy()
-        X = np.frombuffer(hb, np.float64, 4 * (N + 1), o["X"]).reshape(4, N + 1).copy()
-        U = np.frombuffer(hb, np.float64, 2 * N, o["U"]).reshape(2, N).copy()
-        return status, u0, X, U
+            io["up"][:] = u_prev
+        rc = self._L.mpcqp_solve_staged(self._ws)
+        if rc != 0:
+            msg = self._L.mpcqp_last_error().decode(errors="replace")
+            if rc == _lib.E_DEVICE:
+                raise _lib.DeviceError(f"mpcqp_solve_staged: {msg}")
+            raise _lib.LibraryError(f"mpcqp_solve_staged failed ({rc}): {msg}")
+        return int(io["status"][0]), io["u0"].copy(), io["X"].copy(), io["U"].copy()
 
-    def _one_buffers(self) -> dict:
-        torch = self._torch
+    _one = None
+
+    def _stage(self) -> dict:
+        """numpy views of the workspace's B=1 staging blocks (allocated by the first mpcqp_stage;
+        an allocation failure raises DeviceError)."""
         N = self.horizon
+        hin, hout = ctypes.c_void_p(), ctypes.c_void_p()
+        offs = (ctypes.c_int32 * 6)()
+        with self._torch.cuda.device(self.device):
+            rc = self._L.mpcqp_stage(self._ws, ctypes.byref(hin), ctypes.byref(hout), offs)
+        if rc != 0:
+            raise _lib.DeviceError(f"mpcqp_stage failed ({rc}): {self._L.mpcqp_last_error().decode(errors='replace')}")
         nin = 4 + 4 * (N + 1) + 2
-        # outputs packed in one byte block: u0 | X | U (float64), status | iters (int32), active (u8)
-        offs = {"u0": 0, "X": 16, "U": 16 + 32 * (N + 1)}
-        offs["status"] = offs["U"] + 16 * N
-        offs["iters"] = offs["status"] + 4
-        offs["active"] = offs["iters"] + 16
-        nout = offs["active"] + 5 * N + 1
-        if os.environ.get("MPCQP_B1_STAGING", "mapped") != "copy":
-            with torch.cuda.device(self.device):
-                hin = _lib.MappedHostBuffer(8 * nin)
-                hout = _lib.MappedHostBuffer(nout)
-            return dict(mapped=True, hin_buf=hin, hout_buf=hout, hin_np=hin.array(np.float64, nin),
-                        hout_np=hout.array(np.uint8, nout), din_ptr=hin.dev.value, dout_ptr=hout.dev.value,
-                        offs=offs)
-        hin = torch.empty(nin, dtype=torch.float64, pin_memory=True)
-        hout = torch.empty(nout, dtype=torch.uint8, pin_memory=True)
-        return dict(mapped=False, hin=hin, hin_np=hin.numpy(),
-                    din=torch.empty(nin, dtype=torch.float64, device=self.device),
-                    hout=hout, hout_np=hout.numpy(), dout=torch.empty(nout, dtype=torch.uint8, device=self.device),
-                    offs=offs)
+        nout = offs[5] + 5 * N + 1
+        fin = np.frombuffer((ctypes.c_double * nin).from_address(hin.value), np.float64)
+        fout = np.frombuffer((ctypes.c_uint8 * nout).from_address(hout.value), np.uint8)
+        return dict(
+            x0=fin[0:4], ref=fin[4:4 + 4 * (N + 1)].reshape(N + 1, 4), up=fin[4 + 4 * (N + 1):],
+            u0=fout[offs[0]:offs[0] + 16].view(np.float64),
+            X=fout[offs[1]:offs[1] + 32 * (N + 1)].view(np.float64).reshape(4, N + 1),
+            U=fout[offs[2]:offs[2] + 16 * N].view(np.float64).reshape(2, N),
+            status=fout[offs[3]:offs[3] + 4].view(np.int32),
+            iters=fout[offs[4]:offs[4] + 16].view(np.int32),
+            active=fout[offs[5]:offs[5] + 5 * N + 1],
+        )
+
+    @property
+    def closed(self) -> bool:
+        return getattr(self, "_ws", None) is None or not self._ws.value
 
     def close(self) -> None:
-        io = getattr(self, "_one", None)
-        if io is not None and io["mapped"]:
-            if self._ws is not None and self._ws.value:
-                self._torch.cuda.synchronize(self.device)  # nothing may still read or write the blocks
-            io["hin_buf"].free()
-            io["hout_buf"].free()
-            self._one = None
+        # the staging blocks belong to the workspace: mpcqp_destroy syncs its stream and frees them
+        self._one = None
         if getattr(self, "_ws", None) is not None and self._ws.value:
             self._L.mpcqp_destroy(self._ws)
             self._ws = ctypes.c_void_p()
@@ -258,10 +257,24 @@ def latency_settings(horizon: int) -> dict:
     return {"polish_from": 25} if horizon <= 31 else {}
 
 
+# OSQP's default Ruiz pass count (this build's default is 1: DESIGN.md §5)
+OSQP_SCALING = 10
+
+
+def _unpolished_fallback(ctrl: BatchedMPCController) -> bool:
+    """The drop-in re-solves a QP its polish did not finish under OSQP's 10 Ruiz passes: with a
+    polished exact optimum the scaling only changes the work, never the result; without one the
+    returned ADMM iterate depends on it.  Method newton has no ADMM iterate."""
+    c = ctrl._cparams
+    return c.scaling != OSQP_SCALING and c.method == _lib.METHOD_ADMM
+
+
 def _single_controller(params, method: str = "admm", **settings) -> BatchedMPCController:
     settings = {**latency_settings(int(params.horizon)), **settings}  # the caller's settings win
     key = _params_key(params, 0 if method == "admm" else 1, settings)
     ctrl = _CACHE.get(key)
+    if ctrl is not None and ctrl.closed:
+        ctrl = None
     if ctrl is None:
         ctrl = BatchedMPCController(params, 1, method=method, **settings)
         _CACHE[key] = ctrl
@@ -291,24 +304,44 @@ class MPCController:
     ) -> Tuple[Optional[FloatArray], Optional[FloatArray], Optional[FloatArray]]:
         # u_init is accepted and ignored, as in the reference (mpc_controller.py:50-51).
         N = int(self._params.horizon)
-        x0 = np.asarray(x0, dtype=float).reshape(1, 4)
+        x0 = np.asarray(x0, dtype=float)
         ref = np.asarray(ref_traj, dtype=float)
         # The reference reads rows 0..N of ref_traj (mpc_controller.py:68,111) after unwrapping
         # the whole yaw column (:59-60); np.unwrap is a prefix operation, so the first N+1 rows
         # unwrap identically on their own.  Fewer rows fail there (ref[N]) and here.
         if ref.ndim != 2 or ref.shape[1] != 4 or ref.shape[0] < N + 1:
             raise ValueError(f"ref_traj must have shape (>= {N + 1}, 4), got {ref.shape}")
-        ref = ref[: N + 1]
-        up = np.zeros((1, 2)) if u_prev is None else np.asarray(u_prev, dtype=float).reshape(1, 2)
-        # A missing library or device fails loudly here (no CPU fallback exists) ...
-        ctrl = _single_controller(self._params, **self._settings)
+        if x0.size != 4:
+            raise ValueError(f"x0 must have 4 entries, got shape {x0.shape}")
+        x0 = x0.reshape(4)
+        up = None if u_prev is None else np.asarray(u_prev, dtype=float).reshape(2)
+        # A missing library or device, or a failed allocation, fails loudly here (no CPU fallback
+        # exists) ...
+        settings = self._settings
+        if "scaling" not in settings and not settings.get("polish", 1):
+            # no polish: the result is the ADMM iterate, which depends on the scaling -> OSQP's own
+            settings = {**settings, "scaling": OSQP_SCALING}
+        ctrl = _single_controller(self._params, **settings)
         try:
-            status, _, X, U = ctrl.solve_one(x0[0], ref, up[0])
+            status, _, X, U = ctrl.solve_one(x0, ref, up)
         except _lib.LibraryError:
-            # ... while a failed launch of the solve maps to (None, None, None), as the
-            # reference maps cp.SolverError (mpc_controller.py:133-135).
+            # ... while a refused or failed launch of the solve maps to (None, None, None), as the
+            # reference maps cp.SolverError (mpc_controller.py:133-135).  A fault that surfaces at
+            # the stream sync is a DeviceError and propagates.
             LOG.exception("GPU failed during MPC solve")
             return None, None, None
+        if status != _lib.SOLVED and _unpolished_fallback(ctrl):
+            # Not the polished exact optimum (the solution then no longer depends on the scaling):
+            # solve again under OSQP's own 10 Ruiz passes, so the returned unpolished iterate and
+            # status are those of the reference's OSQP settings (mpc_controller.py:119-132).  (The
+            # converse -- one pass polishes a QP that ten passes would leave unpolished -- returns
+            # the exact optimum; it needs a max_iter far below the reference's 60000.)
+            ctrl = _single_controller(self._params, **{**settings, "scaling": OSQP_SCALING})
+            try:
+                status, _, X, U = ctrl.solve_one(x0, ref, up)
+            except _lib.LibraryError:
+                LOG.exception("GPU failed during MPC solve")
+                return None, None, None
         if status == _lib.NUMERICAL_ERROR:
             LOG.error("MPC solve failed with a numerical error")
             return None, None, None

@@ -7,6 +7,8 @@ is kept for API compatibility with the reference module.
 """
 from __future__ import annotations
 
+import math
+
 import numpy as np
 import numpy.typing as npt
 
@@ -15,13 +17,19 @@ Control = npt.NDArray[np.float64]
 
 
 def f_discrete(x: State, u: Control, dt: float, wheelbase_px: float) -> State:
-    """Forward Euler integration of the bicycle model (``vehicle_model.py:11-21``)."""
+    """Forward Euler integration of the bicycle model (``vehicle_model.py:11-21``).
+
+    The same IEEE operations in the same order as the reference.  cos / sin of one float64 are
+    numpy's libm calls, so ``math.cos`` / ``math.sin`` return the same bits (a plain call instead of
+    a ufunc dispatch: this runs once per closed-loop step); ``np.tan`` is numpy's own SIMD kernel,
+    which differs from libm's tan in the last ulp on ~0.5 % of arguments, so it stays.
+    ``tests/test_host.py`` holds the result to the reference's bit for bit (``vehicle.npz``)."""
     xk, yk, yaw, v = x
     a, delta = u
     return np.array(
         [
-            xk + dt * v * np.cos(yaw),
-            yk + dt * v * np.sin(yaw),
+            xk + dt * v * math.cos(yaw),
+            yk + dt * v * math.sin(yaw),
             yaw + dt * (v / wheelbase_px) * np.tan(delta),
             v + dt * a,
         ],

@@ -130,6 +130,8 @@ class TrajectoryTracker:
             elif self._params is not None:
                 params = self._params
             else:
+                LOG.warning("step() before any track() and without params or map_resolution: assuming "
+                            "map_resolution=%s (MapConfig's default) for the px/m scaling", DEFAULT_MAP_RESOLUTION)
                 params = self._params = self.mpc.to_parameters(DEFAULT_MAP_RESOLUTION)
         u0, Xp, _ = self._solve_with_relaxation(state, ref_window, u_prev, params)
         if u0 is None or Xp is None:

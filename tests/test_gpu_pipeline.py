@@ -41,8 +41,8 @@ def test_tracker_reproduces_reference_closed_loop(cuda, golden, N, sim_steps, se
     """BASELINE config 1 (N=10, 100 steps) and the code default (N=15): the reference's
     TrajectoryTracker loop (closed_loop.npz, exact solve substituted for OSQP) is reproduced
     step for step with every QP solved on the GPU: under the B=1 drop-in's latency schedule
-    ({}: mpc_controller.latency_settings), the batch default (150) and another, all of which reach
-    the same exact optimum."""
+    ({}: mpc_controller.latency_settings, polish_from 25) and under polish_from 150 and 50, all of
+    which reach the same exact optimum."""
     from mpcqp.config import MPCConfig, VizConfig
     from mpcqp.pipeline.control_stage import TrajectoryTracker
 
@@ -128,29 +128,67 @@ def test_batched_controller_reuses_device_inputs(cuda):
     ctrl.close()
 
 
-@pytest.mark.parametrize("staging", ["mapped", "copy"])
-def test_solve_one_equals_solve_batch(cuda, monkeypatch, staging):
+def test_solve_one_equals_solve_batch(cuda):
     """The B=1 drop-in (BatchedMPCController.solve_one, behind MPCController.solve) returns
     exactly what solve_batch returns for the same QP, at a fused (N = 20) and a long (N = 40)
-    horizon, including the unsolvable case's status: kernels reading and writing mapped host
-    memory in place, and the staged variant (one copy each way)."""
-    monkeypatch.setenv("MPCQP_B1_STAGING", staging)
+    horizon, including the unsolvable case's status: the staged path (mpcqp_stage /
+    mpcqp_solve_staged: the kernels read and write the workspace's mapped host blocks in place,
+    on its private stream), with windows longer than N + 1 rows and u_prev omitted."""
     from mpcqp import _lib, scenarios
     from mpcqp.config import MPCConfig
     from mpcqp.control.mpc_controller import BatchedMPCController
 
     for N in (20, 40):
-        b = scenarios.config3(4, horizon=N, seed=11)
+        b = scenarios.config3(5, horizon=N, seed=11)
         ref = b.ref.copy()
         ref[3, 2:, 0] = np.nan  # status numerical_error
-        ctrl = BatchedMPCController(MPCConfig(horizon=N).to_parameters(0.8), 4, device="cuda:0")
-        sol = ctrl.solve_batch(b.x0, ref, b.u_prev)
+        up = b.u_prev.copy()
+        up[4] = 0.0
+        ctrl = BatchedMPCController(MPCConfig(horizon=N).to_parameters(0.8), 5, device="cuda:0")
+        sol = ctrl.solve_batch(b.x0, ref, up)
         st, U, X = sol.status.cpu().numpy(), sol.U.cpu().numpy(), sol.X.cpu().numpy()
-        for q in range(4):
-            status, u0, Xq, Uq = ctrl.solve_one(b.x0[q], ref[q], b.u_prev[q])
-            assert ctrl._one["mapped"] == (staging == "mapped")
+        for q in range(5):
+            longer = np.vstack([ref[q], ref[q][-1:] + 1.0])  # an extra row the solve must not read
+            status, u0, Xq, Uq = ctrl.solve_one(b.x0[q], longer, None if q == 4 else up[q])
+            assert ctrl._one is not None
             assert status == st[q]
             if status == _lib.SOLVED:
                 assert np.array_equal(Uq, U[q]) and np.array_equal(Xq, X[q]) and np.array_equal(u0, U[q][:, 0])
         assert st[3] == _lib.NUMERICAL_ERROR
         ctrl.close()
+
+
+def test_drop_in_unpolished_result_is_osqp_scaled(cuda):
+    """A QP the drop-in does not finish with the polished exact optimum (here ADMM capped at
+    max_iter = 50) is solved again under OSQP's 10 Ruiz passes: MPCController then returns exactly
+    what a scaling = 10 solve of the same QP returns, so an unpolished result does not depend on this
+    build's one-pass default.  A polished QP returns the exact optimum, which no scaling
+    changes.  With the polish off, every drop-in solve runs OSQP's 10 passes."""
+    from mpcqp import _lib, scenarios
+    from mpcqp.config import MPCConfig
+    from mpcqp.control.mpc_controller import BatchedMPCController, MPCController
+
+    N = 15
+    b = scenarios.config3(24, horizon=N, seed=3)
+    params = MPCConfig(horizon=N).to_parameters(0.8)
+    for capped in (dict(max_iter=50, polish_from=0, polish_near=0.0),
+                   dict(max_iter=50, polish=0, polish_from=0, polish_near=0.0)):
+        res = {}
+        for sc in (1, 10):
+            c = BatchedMPCController(params, 24, device="cuda:0", scaling=sc, **capped)
+            sol = c.solve_batch(b.x0, b.ref, b.u_prev)
+            res[sc] = (sol.status.cpu().numpy().copy(), sol.U.cpu().numpy().copy())
+            c.close()
+        st1, U1 = res[1]
+        st10, U10 = res[10]
+        polished = (st1 == _lib.SOLVED) & bool(capped.get("polish", 1))
+        assert (~polished).any()  # the fallback case occurs
+        if capped.get("polish", 1):
+            assert polished.any()
+        for q in range(24):
+            u0, X, Uq = MPCController(params, **capped).solve(b.x0[q], b.ref[q], u_prev=b.u_prev[q])
+            exp_st, exp_U = (st1[q], U1[q]) if polished[q] else (st10[q], U10[q])
+            if exp_st in (_lib.SOLVED, _lib.SOLVED_INACCURATE):
+                assert Uq is not None and np.array_equal(Uq, exp_U), q
+            else:
+                assert Uq is None, q

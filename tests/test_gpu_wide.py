@@ -95,7 +95,8 @@ def test_long_horizons_bit_exact_with_c_restatement(cuda, N, settings):
     assert np.array_equal(out["active"], ref["active"])
 
 
-@pytest.mark.parametrize("N,settings", [(32, {}), (40, {}), (48, {"polish_from": 0, "polish_near": 0.0}), (63, {})])
+@pytest.mark.parametrize("N,settings", [(32, {}), (33, {}), (40, {}), (41, {}),
+                                        (48, {"polish_from": 0, "polish_near": 0.0}), (52, {}), (56, {}), (63, {})])
 def test_long_horizons_fast_mode_against_c_restatement(cuda, N, settings):
     """The default (fast) long-horizon mode (the mid kernel): the same optimum, statuses, active sets
     and all four counters as the C restatement on every QP (its tree-order sums round differently,
@@ -216,9 +217,9 @@ def test_mpc_controller_drop_in_at_horizon_40(cuda):
     assert X.shape == (4, 41) and U.shape == (2, 40)
 
 
-@pytest.mark.parametrize("N", [40, 80])
+@pytest.mark.parametrize("N", [40, 56, 80])
 def test_fleet_at_long_horizons(cuda, N):
-    """The device closed loop at N = 40 and 80 (k_fleet_build -- in chunks of 64 window rows at
+    """The device closed loop at N = 40, 56 (the mid kernel's 4-part bucket) and 80 (k_fleet_build -- in chunks of 64 window rows at
     80 -- + the long-horizon solve) against the oracle's restatement of control_stage.py:84-150 on
     the same plans."""
     import mpc_oracle as mo

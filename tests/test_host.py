@@ -35,7 +35,7 @@ def test_library_exports_every_header_symbol():
         assert hasattr(handle, name), f"{name} declared in include/mpcqp.h but not exported"
     assert set(decls) == set(_lib_mod.exported_symbols())
     L = _lib_mod.lib()
-    assert L.mpcqp_version() == _lib_mod.ABI_VERSION == 6
+    assert L.mpcqp_version() == _lib_mod.ABI_VERSION == 7
     assert L.mpcqp_num_rows(20) == 101
     assert L.mpcqp_model_stride(20) % 8 == 0
 

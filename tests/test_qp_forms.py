@@ -110,3 +110,25 @@ def test_exact_optimum_is_kkt_on_reference_matrices(forms, stride):
                          lsmr_tol="auto", method="bvls")
         stat = np.abs(c["A"][act].T @ fit.x + g).max()
         assert stat <= 1e-8 * max(1.0, np.abs(g).max()), f"{c['tag']}: stationarity residual {stat:.3e}"
+
+
+def test_ruiz_passes_do_not_change_the_polished_optimum(forms):
+    """This build runs one Ruiz pass by default where OSQP runs 10.  On every one of
+    the reference's 189 QPs both settings end polished (status 1) at the same exact optimum: identical
+    active sets, U within 1e-9 of each other and of the exact solver.  (The algorithm restated in C,
+    oracle/mpcqp_cpu.c, whose counters the GPU kernels match QP for QP.)  An unpolished result would
+    depend on the scaling: the B=1 drop-in then re-solves under 10 passes
+    (tests/test_gpu_pipeline.py::test_drop_in_unpolished_result_is_osqp_scaled)."""
+    import cpu_solver
+
+    for i in range(len(forms["tags"])):
+        c = _case(forms, i)
+        ex = mo.solve_exact(c["params"], c["x0"], c["window"], c["u_prev"])
+        outs = [cpu_solver.cpu_solve(c["params"], c["x0"][None], c["window"][None], c["u_prev"][None], nthreads=1,
+                                     scaling=sc) for sc in (1, 10)]
+        for o in outs:
+            assert int(o["status"][0]) == 1, c["tag"]
+            assert np.array_equal(o["active"][0], ex.active), c["tag"]
+            err = np.abs(o["U"][0] - ex.Umat).max() / max(1.0, np.abs(ex.Umat).max())
+            assert err <= 1e-9, (c["tag"], err)
+        assert np.array_equal(outs[0]["active"], outs[1]["active"]), c["tag"]

@@ -18,6 +18,7 @@ import argparse
 import collections
 import csv
 import json
+import sys
 from pathlib import Path
 
 SOLVE = ("k_solve",)
@@ -35,11 +36,30 @@ def per_kernel(path: Path, N: int) -> dict:
     return {k: sum(v) / len(v) for k, v in acc.items()}
 
 
+def measurement_keys(N: int, sets: list) -> dict:
+    """bench.settings_key / bench.lib_key of the measured run (run this with the .so the passes ran)."""
+    root = Path(__file__).resolve().parents[1]
+    sys.path[:0] = [str(root), str(root / "rrt-mpc_amd")]
+    import bench
+    from mpcqp import _lib
+    from mpcqp.config import MPCConfig
+
+    extra = {}
+    for kv in sets:
+        k, v = kv.split("=", 1)
+        extra[k] = float(v) if "." in v or "e" in v else int(v)
+    cp = _lib.to_c_params(MPCConfig(horizon=N).to_parameters(0.8), **extra)
+    return {"settings_key": bench.settings_key(cp), "lib_key": bench.lib_key(),
+            "solver_settings": bench.solver_settings(cp)}
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("out_dir")
     ap.add_argument("--N", type=int, default=20)
     ap.add_argument("--B", type=int, default=4096)
+    ap.add_argument("--set", action="append", default=[], metavar="KEY=VALUE",
+                    help="solver settings the passes ran with (bench.py --set), default: the library's")
     a = ap.parse_args()
     d = Path(a.out_dir)
     c = {}
@@ -92,6 +112,8 @@ def main() -> None:
                                         / sq["SQ_WAVES"]) if sq.get("SQ_WAVES") else None,
             "valu_insts_per_wave": sq["SQ_INSTS_VALU"] / sq["SQ_WAVES"] if sq.get("SQ_WAVES") and "SQ_INSTS_VALU" in sq else None,
         }
+    # bench.py attaches this entry to its line only when the run's settings and kernel library match
+    out[f"N{N}_B{B}"].update(measurement_keys(N, a.set))
     print(json.dumps(out, indent=1))
 
 
