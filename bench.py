@@ -657,7 +657,7 @@ def main() -> int:
     stream = torch.cuda.current_stream(device)
     s = ctypes.c_void_p(stream.cuda_stream)
     events = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
-    # K1 is fused into the solve kernel (N < 32, fast mode, no debug state): mpcqp_build enqueues
+    # K1 is fused into the solve kernel (N <= 32, fast mode, no debug state): mpcqp_build enqueues
     # nothing, so one event pair brackets the step's only kernel (a middle event would add its own
     # ~5 us packet to every step); otherwise k_build and k_solve are timed apart
     fused = N < _lib.WIDE_MIN_HORIZON and not extra.get("reproducible", 0) and not extra.get("debug_state", 0)

@@ -48,10 +48,10 @@ extern "C" {
                                     an earlier kernel faulted; the device context is unusable) */
 
 #define MPCQP_MAX_HORIZON 1024   /* per-QP workspace 16 (2N)^2 bytes: 67 MB at N = 1024 */
-#define MPCQP_WIDE_MIN_HORIZON 32 /* N <= 31: one wave per QP (2N variables on the lanes, the KKT
-                                     inverse in registers); N >= 32: one workgroup per QP */
-#define MPCQP_MID_MAX_HORIZON 63  /* 32 <= N <= 63 (fast mode): 4 x 1-2 waves per QP, the KKT inverse's
-                                     rows split in four column parts over their registers; beyond, and in
+#define MPCQP_WIDE_MIN_HORIZON 33 /* N <= 32: one wave per QP (2N <= 64 variables on the lanes, the KKT
+                                     inverse in registers); N >= 33: one workgroup per QP */
+#define MPCQP_MID_MAX_HORIZON 63  /* 33 <= N <= 63 (fast mode): 2-4 x 1-2 waves per QP, the KKT inverse's
+                                     rows split in column parts over their registers; beyond, and in
                                      reproducible mode, 256 threads restating the C code */
 
 /* per-QP status codes (mirror OSQP's; mpc_controller.py:137 accepts 1 and 2).
@@ -250,7 +250,7 @@ int mpcqp_fleet_run(mpcqp_ws* nominal, mpcqp_ws* relaxed, const mpcqp_fleet* f, 
  * X, and status / u0 of each vehicle's last step) equals mpcqp_fleet_run's bit for bit (the mask
  * scratch keeps each vehicle's last-step masks).  The loop does not write debug state.  Vehicles leave
  * the loop at the goal, on abort or out of steps, so one call with steps = max_steps runs every
- * vehicle to its end.  Horizons N <= 31 in fast mode without debug_state run the fused kernel;
+ * vehicle to its end.  Horizons N <= 32 in fast mode without debug_state run the fused kernel;
  * other parameter blocks (mid / long horizons, reproducible or debug_state) are executed by
  * mpcqp_fleet_run's graph path. */
 int mpcqp_fleet_loop(mpcqp_ws* nominal, mpcqp_ws* relaxed, const mpcqp_fleet* f, int steps, void* stream);

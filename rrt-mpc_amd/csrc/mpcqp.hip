@@ -84,7 +84,8 @@ const mpcqp::launcher_t kLaunchers[MPCQP_WIDE_MIN_HORIZON] = {
     nullptr,     MPCQP_L(1),  MPCQP_L(2),  MPCQP_L(3),  MPCQP_L(4),  MPCQP_L(5),  MPCQP_L(6),  MPCQP_L(7),
     MPCQP_L(8),  MPCQP_L(9),  MPCQP_L(10), MPCQP_L(11), MPCQP_L(12), MPCQP_L(13), MPCQP_L(14), MPCQP_L(15),
     MPCQP_L(16), MPCQP_L(17), MPCQP_L(18), MPCQP_L(19), MPCQP_L(20), MPCQP_L(21), MPCQP_L(22), MPCQP_L(23),
-    MPCQP_L(24), MPCQP_L(25), MPCQP_L(26), MPCQP_L(27), MPCQP_L(28), MPCQP_L(29), MPCQP_L(30), MPCQP_L(31)};
+    MPCQP_L(24), MPCQP_L(25), MPCQP_L(26), MPCQP_L(27), MPCQP_L(28), MPCQP_L(29), MPCQP_L(30), MPCQP_L(31),
+    MPCQP_L(32)};
 #undef MPCQP_L
 #ifdef MPCQP_ONLY_N
 #define MPCQP_F(N) ((N) == MPCQP_ONLY_N ? &mpcqp::launch_fleet_loop<MPCQP_ONLY_N> : nullptr)
@@ -95,7 +96,8 @@ const mpcqp::fleet_loop_t kFleetLoops[MPCQP_WIDE_MIN_HORIZON] = {
     nullptr,     MPCQP_F(1),  MPCQP_F(2),  MPCQP_F(3),  MPCQP_F(4),  MPCQP_F(5),  MPCQP_F(6),  MPCQP_F(7),
     MPCQP_F(8),  MPCQP_F(9),  MPCQP_F(10), MPCQP_F(11), MPCQP_F(12), MPCQP_F(13), MPCQP_F(14), MPCQP_F(15),
     MPCQP_F(16), MPCQP_F(17), MPCQP_F(18), MPCQP_F(19), MPCQP_F(20), MPCQP_F(21), MPCQP_F(22), MPCQP_F(23),
-    MPCQP_F(24), MPCQP_F(25), MPCQP_F(26), MPCQP_F(27), MPCQP_F(28), MPCQP_F(29), MPCQP_F(30), MPCQP_F(31)};
+    MPCQP_F(24), MPCQP_F(25), MPCQP_F(26), MPCQP_F(27), MPCQP_F(28), MPCQP_F(29), MPCQP_F(30), MPCQP_F(31),
+    MPCQP_F(32)};
 #undef MPCQP_F
 
 // per-QP doubles of the solver state buffer (debug state of the one-wave kernel, the workspace
@@ -108,8 +110,7 @@ size_t ws_state_stride(int N, bool wide) {
 }
 
 void launch_mid(hipStream_t s, const Launch& L) {
-  switch (mpcqp::mid_bucket(L.p->horizon)) {
-    case 32: mpcqp::launch_solve_mid<32>(s, L); break;
+  switch (mpcqp::mid_bucket(L.p->horizon)) {  // N >= 33: N = 32 runs the one-wave kernel
     case 40: mpcqp::launch_solve_mid<40>(s, L); break;
     case 48: mpcqp::launch_solve_mid<48>(s, L); break;
     case 56: mpcqp::launch_solve_mid<56>(s, L); break;

@@ -281,7 +281,7 @@ typedef void (*launcher_t)(hipStream_t, const Launch&);
 // mpcqp_part.hip objects (parallel build) or in mpcqp.hip itself (MPCQP_ONLY_N dev builds).
 template <int N>
 void launch_solve(hipStream_t s, const Launch& L);
-// the fused closed loop of a fleet (k_fleet_loop<N>, mpcqp_solve.h; N <= 31, fast mode): `steps`
+// the fused closed loop of a fleet (k_fleet_loop<N>, mpcqp_solve.h; N <= 32, fast mode): `steps`
 // loop steps of every RUNNING vehicle in one launch
 // The config-5 replan trigger inside the fused loop (mpcqp_swarm_loop): after each step a RUNNING
 // vehicle farther than replan_distance from ref[path_idx], or an ABORTED one, with replans left leaves
@@ -310,7 +310,7 @@ size_t wide_stride(int horizon);
 // workspace (mid_stride(N) doubles per QP: the scaled Hessian)
 template <int NT>
 void launch_solve_mid(hipStream_t s, const Launch& L);
-inline int mid_bucket(int N) { return N <= 32 ? 32 : (N <= 40 ? 40 : (N <= 48 ? 48 : (N <= 56 ? 56 : 64))); }
+inline int mid_bucket(int N) { return N <= 40 ? 40 : (N <= 48 ? 48 : (N <= 56 ? 56 : 64)); }  // N >= 33
 inline size_t mid_stride(int N) { return (size_t)2 * mid_bucket(N) * 128; }
 // the solve of this parameter block runs a workgroup-per-QP kernel (long horizon or reproducible)
 bool wide_solve(const mpcqp_params& p);

@@ -162,4 +162,9 @@ template void launch_solve<31>(hipStream_t, const Launch&);
 template void launch_fleet_loop<31>(hipStream_t, const mpcqp_params*, const mpcqp_fleet&, int,
                                            const LoopTrigger&);
 #endif
+#if MPCQP_PART_LO <= 32 && 32 <= MPCQP_PART_HI
+template void launch_solve<32>(hipStream_t, const Launch&);
+template void launch_fleet_loop<32>(hipStream_t, const mpcqp_params*, const mpcqp_fleet&, int,
+                                           const LoopTrigger&);
+#endif
 }  // namespace mpcqp

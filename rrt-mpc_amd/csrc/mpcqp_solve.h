@@ -508,10 +508,116 @@ __device__ __forceinline__ bool setup_qp(const mpcqp_params& p, int b, const dou
   // mu_m = W_m s_m + A_m' mu_{m+1};  H[(i,c'), col] = (B_i e_c')' mu_{i+1}
   // The column stays in registers (Pc) through the scaling; static indices need the m loop
   // fully unrolled.
+  // At n = 64 (N = 32) no lane is left over for g: the second branch.
   double Pc[n];
+  if constexpr (n < kWave) {
 #pragma unroll
-  for (int i = 0; i < n; ++i) Pc[i] = 0.0;
-  if (lane <= n) {
+    for (int i = 0; i < n; ++i) Pc[i] = 0.0;
+    if (lane <= n) {
+      double Q[4][4], QN[4][4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          Q[i][j] = 0.5 * (p.q[4 * i + j] + p.q[4 * j + i]);
+          QN[i][j] = 0.5 * (p.q_terminal[4 * i + j] + p.q_terminal[4 * j + i]);
+        }
+      const int j = lane >> 1;
+      const bool gcol = lane == n;
+      const double sj = gcol ? 0.0 : si[j];
+      const double pa0 = gcol ? 0.0 : sm.pre[0][j + 1], pg0 = gcol ? 0.0 : sm.pre[2][j + 1];
+      const double bj = (!gcol && j + 1 < N) ? be[j + 1] : 0.0, ej = (!gcol && j + 1 < N) ? et[j + 1] : 0.0;
+      double mu0 = 0.0, mu1 = 0.0, mu2 = 0.0;
+#pragma unroll
+      for (int m = N; m >= 1; --m) {
+        double s0, s1, s2, s3;
+        if (gcol) {
+          s0 = sm.err[m][0];
+          s1 = sm.err[m][1];
+          s2 = sm.err[m][2];
+          s3 = sm.err[m][3];
+        } else if (m > j) {
+          if (cc == 0) {  // v_{j+1}: itself at m = j+1, the positions from m = j+2 on
+            s0 = m >= j + 2 ? bj : 0.0;
+            s1 = m >= j + 2 ? ej : 0.0;
+            s2 = 0.0;
+            s3 = m == j + 1 ? 1.0 : 0.0;
+          } else {
+            s0 = sj * (sm.pre[0][m] - pa0);
+            s1 = sj * (sm.pre[2][m] - pg0);
+            s2 = sj;
+            s3 = 0.0;
+          }
+        } else {
+          s0 = s1 = s2 = s3 = 0.0;
+        }
+        const bool term = m == N;
+        auto W = [&](int i, int k) -> double { return term ? QN[i][k] : Q[i][k]; };
+        const double w0 = W(0, 0) * s0 + W(0, 1) * s1 + W(0, 2) * s2 + W(0, 3) * s3;
+        const double w1 = W(1, 0) * s0 + W(1, 1) * s1 + W(1, 2) * s2 + W(1, 3) * s3;
+        const double w2 = W(2, 0) * s0 + W(2, 1) * s1 + W(2, 2) * s2 + W(2, 3) * s3;
+        const double w3 = W(3, 0) * s0 + W(3, 1) * s1 + W(3, 2) * s2 + W(3, 3) * s3;
+        // row v_m: its own cost term + the positions after it; row delta_{m-1}: si * heading adjoint
+        double ha;
+        if (m < N) {
+          const double m0 = mu0, m1 = mu1;
+          ha = w3 + (be[m] * m0 + et[m] * m1);
+          mu0 = w0 + m0;
+          mu1 = w1 + m1;
+          mu2 = w2 + (mu2 + al[m] * m0 + ga[m] * m1);
+        } else {
+          ha = w3;
+          mu0 = w0;
+          mu1 = w1;
+          mu2 = w2;
+        }
+        const double hd = si[m - 1] * mu2;
+        if (gcol) {
+          sm.g[2 * (m - 1)] = ha;
+          sm.g[2 * (m - 1) + 1] = hd;
+        } else {
+          Pc[2 * (m - 1)] = ha;
+          Pc[2 * (m - 1) + 1] = hd;
+        }
+      }
+      // input cost sum_k U_k' R U_k with a_k = (v_{k+1} - v_k)/dt: a band of column `lane`
+      const double r00 = 0.5 * (p.r[0] + p.r[0]) / (dt * dt), r10 = 0.5 * (p.r[2] + p.r[1]) / dt;
+      const double r11 = 0.5 * (p.r[3] + p.r[3]);
+      if (gcol) {  // the v_0 = x0[3] end of a_0
+        sm.g[0] += -x0[3] * r00;
+        sm.g[1] += -x0[3] * r10;
+      } else {
+#pragma unroll
+        for (int i = 0; i < n; ++i) {
+          const int d = i - lane;
+          double add = 0.0;
+          if (cc == 0) {
+            if (d == 0) add = lane + 2 < n ? 2.0 * r00 : r00;
+            if (d == 2 || d == -2) add = -r00;
+            if (d == 1) add = r10;
+            if (d == 3) add = -r10;
+          } else {
+            if (d == 0) add = r11;
+            if (d == -1) add = r10;
+            if (d == -3) add = -r10;
+          }
+          Pc[i] += add;
+        }
+      }
+    }
+    __syncthreads();
+    if (!act)
+#pragma unroll
+      for (int i = 0; i < n; ++i) Pc[i] = 0.0;  // lane n carried g
+  } else {
+    // n = 64 (N = 32): every lane holds a column, so g takes a second pass of the same recursion,
+    // wave-uniform (its inputs are the free-response errors alone), stored by lane 0.  Unrolled by
+    // template (a #pragma unroll of this body stops at clang's threshold, and Pc would then be
+    // indexed dynamically: scratch memory).  Each step's LDS reads and lane compares stay in their
+    // step (hoisted, they spill the column's 128 registers), and the input-cost band is added to the
+    // step's two rows right there (the same sum ha + band as the band loop above).
+#pragma unroll
+    for (int i = 0; i < n; ++i) Pc[i] = 0.0;
     double Q[4][4], QN[4][4];
 #pragma unroll
     for (int i = 0; i < 4; ++i)
@@ -520,93 +626,95 @@ __device__ __forceinline__ bool setup_qp(const mpcqp_params& p, int b, const dou
         Q[i][j] = 0.5 * (p.q[4 * i + j] + p.q[4 * j + i]);
         QN[i][j] = 0.5 * (p.q_terminal[4 * i + j] + p.q_terminal[4 * j + i]);
       }
-    const int j = lane >> 1;
-    const bool gcol = lane == n;
-    const double sj = gcol ? 0.0 : si[j];
-    const double pa0 = gcol ? 0.0 : sm.pre[0][j + 1], pg0 = gcol ? 0.0 : sm.pre[2][j + 1];
-    const double bj = (!gcol && j + 1 < N) ? be[j + 1] : 0.0, ej = (!gcol && j + 1 < N) ? et[j + 1] : 0.0;
-    double mu0 = 0.0, mu1 = 0.0, mu2 = 0.0;
-#pragma unroll
-    for (int m = N; m >= 1; --m) {
-      double s0, s1, s2, s3;
-      if (gcol) {
-        s0 = sm.err[m][0];
-        s1 = sm.err[m][1];
-        s2 = sm.err[m][2];
-        s3 = sm.err[m][3];
-      } else if (m > j) {
-        if (cc == 0) {  // v_{j+1}: itself at m = j+1, the positions from m = j+2 on
-          s0 = m >= j + 2 ? bj : 0.0;
-          s1 = m >= j + 2 ? ej : 0.0;
-          s2 = 0.0;
-          s3 = m == j + 1 ? 1.0 : 0.0;
-        } else {
-          s0 = sj * (sm.pre[0][m] - pa0);
-          s1 = sj * (sm.pre[2][m] - pg0);
-          s2 = sj;
-          s3 = 0.0;
-        }
-      } else {
-        s0 = s1 = s2 = s3 = 0.0;
-      }
-      const bool term = m == N;
-      auto W = [&](int i, int k) -> double { return term ? QN[i][k] : Q[i][k]; };
-      const double w0 = W(0, 0) * s0 + W(0, 1) * s1 + W(0, 2) * s2 + W(0, 3) * s3;
-      const double w1 = W(1, 0) * s0 + W(1, 1) * s1 + W(1, 2) * s2 + W(1, 3) * s3;
-      const double w2 = W(2, 0) * s0 + W(2, 1) * s1 + W(2, 2) * s2 + W(2, 3) * s3;
-      const double w3 = W(3, 0) * s0 + W(3, 1) * s1 + W(3, 2) * s2 + W(3, 3) * s3;
-      // row v_m: its own cost term + the positions after it; row delta_{m-1}: si * heading adjoint
-      double ha;
-      if (m < N) {
-        const double m0 = mu0, m1 = mu1;
-        ha = w3 + (be[m] * m0 + et[m] * m1);
-        mu0 = w0 + m0;
-        mu1 = w1 + m1;
-        mu2 = w2 + (mu2 + al[m] * m0 + ga[m] * m1);
-      } else {
-        ha = w3;
-        mu0 = w0;
-        mu1 = w1;
-        mu2 = w2;
-      }
-      const double hd = si[m - 1] * mu2;
-      if (gcol) {
-        sm.g[2 * (m - 1)] = ha;
-        sm.g[2 * (m - 1) + 1] = hd;
-      } else {
-        Pc[2 * (m - 1)] = ha;
-        Pc[2 * (m - 1) + 1] = hd;
-      }
-    }
-    // input cost sum_k U_k' R U_k with a_k = (v_{k+1} - v_k)/dt: a band of column `lane`
     const double r00 = 0.5 * (p.r[0] + p.r[0]) / (dt * dt), r10 = 0.5 * (p.r[2] + p.r[1]) / dt;
     const double r11 = 0.5 * (p.r[3] + p.r[3]);
-    if (gcol) {  // the v_0 = x0[3] end of a_0
-      sm.g[0] += -x0[3] * r00;
-      sm.g[1] += -x0[3] * r10;
-    } else {
-#pragma unroll
-      for (int i = 0; i < n; ++i) {
-        const int d = i - lane;
-        double add = 0.0;
-        if (cc == 0) {
-          if (d == 0) add = lane + 2 < n ? 2.0 * r00 : r00;
-          if (d == 2 || d == -2) add = -r00;
-          if (d == 1) add = r10;
-          if (d == 3) add = -r10;
+#pragma nounroll
+    for (int gpass = 0; gpass < 2; ++gpass) {
+      const int j = lane >> 1;
+      const bool gcol = gpass == 1;
+      const double sj = gcol ? 0.0 : si[j];
+      const double pa0 = gcol ? 0.0 : sm.pre[0][j + 1], pg0 = gcol ? 0.0 : sm.pre[2][j + 1];
+      const double bj = (!gcol && j + 1 < N) ? be[j + 1] : 0.0, ej = (!gcol && j + 1 < N) ? et[j + 1] : 0.0;
+      double mu0 = 0.0, mu1 = 0.0, mu2 = 0.0;
+      Unroll<0, N>::run([&](auto mc) __attribute__((always_inline)) {
+        constexpr int m = N - decltype(mc)::value;
+        double s0, s1, s2, s3;
+        if (gcol) {
+          s0 = sm.err[m][0];
+          s1 = sm.err[m][1];
+          s2 = sm.err[m][2];
+          s3 = sm.err[m][3];
+        } else if (m > j) {
+          if (cc == 0) {
+            s0 = m >= j + 2 ? bj : 0.0;
+            s1 = m >= j + 2 ? ej : 0.0;
+            s2 = 0.0;
+            s3 = m == j + 1 ? 1.0 : 0.0;
+          } else {
+            s0 = sj * (sm.pre[0][m] - pa0);
+            s1 = sj * (sm.pre[2][m] - pg0);
+            s2 = sj;
+            s3 = 0.0;
+          }
         } else {
-          if (d == 0) add = r11;
-          if (d == -1) add = r10;
-          if (d == -3) add = -r10;
+          s0 = s1 = s2 = s3 = 0.0;
         }
-        Pc[i] += add;
+        const bool term = m == N;
+        auto W = [&](int i, int k) -> double { return term ? QN[i][k] : Q[i][k]; };
+        const double w0 = W(0, 0) * s0 + W(0, 1) * s1 + W(0, 2) * s2 + W(0, 3) * s3;
+        const double w1 = W(1, 0) * s0 + W(1, 1) * s1 + W(1, 2) * s2 + W(1, 3) * s3;
+        const double w2 = W(2, 0) * s0 + W(2, 1) * s1 + W(2, 2) * s2 + W(2, 3) * s3;
+        const double w3 = W(3, 0) * s0 + W(3, 1) * s1 + W(3, 2) * s2 + W(3, 3) * s3;
+        double ha;
+        if (m < N) {
+          const double m0 = mu0, m1 = mu1;
+          ha = w3 + (be[m] * m0 + et[m] * m1);
+          mu0 = w0 + m0;
+          mu1 = w1 + m1;
+          mu2 = w2 + (mu2 + al[m] * m0 + ga[m] * m1);
+        } else {
+          ha = w3;
+          mu0 = w0;
+          mu1 = w1;
+          mu2 = w2;
+        }
+        const double hd = si[m - 1] * mu2;
+        // two conditions, not an if/else: merged into one store through a select of the two
+        // addresses, the column would be addressed through a generic pointer (scratch memory)
+        if (gcol && lane == 0) {
+          sm.g[2 * (m - 1)] = ha;
+          sm.g[2 * (m - 1) + 1] = hd;
+        }
+        if (!gcol) {
+          int ln = lane;  // opaque per step: the band's compares are not hoisted out of the pass loop
+          asm volatile("" : "+v"(ln));
+          auto band = [&](int i) -> double {  // the band entry of row i in column ln
+            const int d = i - ln;
+            double add = 0.0;
+            if (cc == 0) {
+              if (d == 0) add = ln + 2 < n ? 2.0 * r00 : r00;
+              if (d == 2 || d == -2) add = -r00;
+              if (d == 1) add = r10;
+              if (d == 3) add = -r10;
+            } else {
+              if (d == 0) add = r11;
+              if (d == -1) add = r10;
+              if (d == -3) add = -r10;
+            }
+            return add;
+          };
+          Pc[2 * (m - 1)] = ha + band(2 * (m - 1));
+          Pc[2 * (m - 1) + 1] = hd + band(2 * (m - 1) + 1);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      });
+      if (gcol && lane == 0) {  // the v_0 = x0[3] end of a_0
+        sm.g[0] += -x0[3] * r00;
+        sm.g[1] += -x0[3] * r10;
       }
     }
+    __syncthreads();
   }
-  __syncthreads();
-  if (!act)
-#pragma unroll
-    for (int i = 0; i < n; ++i) Pc[i] = 0.0;  // lane n carried g
   T.end(1);
   T.begin();
 

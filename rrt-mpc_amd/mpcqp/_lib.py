@@ -18,7 +18,7 @@ LIB_PATH = Path(os.environ.get("MPCQP_LIB", Path(__file__).resolve().parent / LI
 
 # constants mirrored from include/mpcqp.h
 MAX_HORIZON = 1024
-WIDE_MIN_HORIZON = 32  # MPCQP_WIDE_MIN_HORIZON: one 256-thread workgroup per QP from here on
+WIDE_MIN_HORIZON = 33  # MPCQP_WIDE_MIN_HORIZON: a workgroup per QP from here on (N <= 32: one wave)
 SOLVED = 1
 SOLVED_INACCURATE = 2
 MAX_ITER_REACHED = -2

@@ -254,7 +254,7 @@ def latency_settings(horizon: int) -> dict:
     at N = 10, 15, 20 and 30.  The horizons past the one-wave kernel keep the default (unmeasured).
     Every schedule ends at the exact optimum; the counters match the C restatement under each
     (tests/test_gpu_parity.py)."""
-    return {"polish_from": 25} if horizon <= 31 else {}
+    return {"polish_from": 25} if horizon <= 32 else {}
 
 
 # OSQP's default Ruiz pass count (this build's default is 1: DESIGN.md §5)

@@ -76,7 +76,7 @@ def closed_loop_settings(horizon: int) -> dict:
     profiles/r03_s14_schedule_fleets.json): `polish_from` 25 against 75 gives -9 / -7 / -10 % at
     100 / 1024 / 4096 vehicles and -5 % on the config-5 swarm.  Past the one-wave kernel the default
     stays (unmeasured)."""
-    return {"polish_from": 25} if horizon <= 31 else {}
+    return {"polish_from": 25} if horizon <= 32 else {}
 
 
 class FleetTracker:

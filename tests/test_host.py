@@ -292,21 +292,22 @@ def test_solver_kernel_resources():
     rec = json.loads(path.read_text())
     res = {int(k): v for k, v in rec.items() if not k.startswith("loop:")}
     loops = {int(k.split(":")[1]): v for k, v in rec.items() if k.startswith("loop:")}
-    assert sorted(res) == list(range(1, 32))
-    assert sorted(loops) == list(range(1, 32))
+    assert sorted(res) == list(range(1, 33))
+    assert sorted(loops) == list(range(1, 33))
     for N, r in loops.items():
         # the fused closed loop (k_fleet_loop<N>) runs the same solver at 2 waves per SIMD; values
         # live across the steps (loop state, output pointers) spill at the step boundary only
         assert r["Occupancy"] >= 2 and r["AGPRs"] == 0, (N, r)
-        assert r["ScratchSize"] <= 512, (N, r)
+        assert r["ScratchSize"] <= (640 if N == 32 else 512), (N, r)
         assert r["LDS"] <= 160 * 1024 // 8, (N, r)
     for N, r in res.items():
         # every horizon at 2 waves per SIMD and 8 workgroups per CU (N >= 24: Pbar packed, <= 18 KB
-        # of LDS); N >= 29 fills
-        # the 256 registers and spills a handful of values outside the inverse (<= 64 bytes)
+        # of LDS); N >= 29 fills the 256 registers and spills a handful of values outside the
+        # inverse (<= 64 bytes); N = 32 (2N = 64: every lane a column, g in a second condensing
+        # pass) spills part of the setup column around that pass (setup only, <= 320 bytes)
         assert r["Occupancy"] >= 2, (N, r)
         assert r["AGPRs"] == 0, (N, r)
-        assert r["ScratchSize"] <= (64 if N >= 29 else 0), (N, r)
+        assert r["ScratchSize"] <= (320 if N == 32 else 64 if N >= 29 else 0), (N, r)
         assert r["LDS"] <= 160 * 1024 // 8, (N, r)  # 8 workgroups = 2 waves on each of 4 SIMDs
 
 
