@@ -76,7 +76,7 @@ def test_newton_method_matches(cuda):
 
 
 @pytest.mark.parametrize("cfg,N,B", [("config2", 20, 1024), ("config3", 10, 1024), ("config3", 24, 1024),
-                                     ("config3", 31, 1024), ("config4", 30, 4096)])
+                                     ("config3", 31, 1024), ("config3", 32, 1024), ("config4", 30, 4096)])
 def test_iteration_indexing_bit_exact_on_product_path(cuda, cfg, N, B):
     """The product kernel (fast mode) against the C restatement on whole batches: all four counters
     (ADMM iterations, polish passes, factorizations, line-search trials), statuses and active sets

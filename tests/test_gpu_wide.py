@@ -98,7 +98,8 @@ def test_long_horizons_bit_exact_with_c_restatement(cuda, N, settings):
 @pytest.mark.parametrize("N,settings", [(32, {}), (33, {}), (40, {}), (41, {}),
                                         (48, {"polish_from": 0, "polish_near": 0.0}), (52, {}), (56, {}), (63, {})])
 def test_long_horizons_fast_mode_against_c_restatement(cuda, N, settings):
-    """The default (fast) long-horizon mode (the mid kernel): the same optimum, statuses, active sets
+    """The default (fast) long-horizon mode (the mid kernel from N = 33, the one-wave kernel at N = 32): the
+    same optimum, statuses, active sets
     and all four counters as the C restatement on every QP (its tree-order sums round differently,
     but no counter decision flips: profiles/r03_s16_iters_agreement.json, 6 x 1024 QPs at N = 32..63)."""
     import cpu_solver
@@ -107,7 +108,9 @@ def test_long_horizons_fast_mode_against_c_restatement(cuda, N, settings):
     batch = scenarios.config3(64, horizon=N, seed=900 + N)
     params = _params(N)
     out, model = _solve_with_model(params, batch.x0, batch.ref, batch.u_prev, **settings)
-    ref = cpu_solver.cpu_solve_models(params, model, **settings)
+    # N = 32 runs the one-wave kernel with K1 fused (no model buffer): the C code from the inputs
+    ref = (cpu_solver.cpu_solve_models(params, model, **settings) if model is not None else
+           cpu_solver.cpu_solve(params, batch.x0, batch.ref, batch.u_prev, **settings))
     assert np.array_equal(out["status"], ref["status"])
     assert np.array_equal(out["active"], ref["active"])
     assert _rel(out["U"], ref["U"]) <= REL_TOL and _rel(out["X"], ref["X"]) <= REL_TOL
