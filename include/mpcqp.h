@@ -192,6 +192,14 @@ int mpcqp_solve(mpcqp_ws* ws, int B, double* u0, double* X, double* U, int32_t* 
  * Replaces the per-call cvxpy build + OSQP solve of MPCController.solve (mpc_controller.py:53-141). */
 int mpcqp_stage(mpcqp_ws* ws, double** in, void** out, int32_t offsets[6]);
 int mpcqp_solve_staged(mpcqp_ws* ws);
+/* The same contract without a launch per call: the first call starts one resident wave on the
+ * workspace's stream that solves the staged QP each time this function raises a request in a
+ * mailbox of mapped host memory, and publishes completion there (the call spins on it).  The wave
+ * leaves after 2 ms without a request, at mpcqp_set_params and at mpcqp_destroy; the next call
+ * starts it again.  While it is resident, a device-wide synchronisation (hipDeviceSynchronize)
+ * waits for it to go idle.  Horizons without the one-wave kernel (N > 32, reproducible, debug
+ * builds) run mpcqp_solve_staged. */
+int mpcqp_solve_served(mpcqp_ws* ws);
 
 /*
  * Closed-loop fleet: V vehicles tracking their own references, one MPC step each per call

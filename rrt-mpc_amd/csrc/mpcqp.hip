@@ -13,6 +13,8 @@
 // problem never leaves the CU (the per-QP state buffer is written only with debug_state).
 // The algorithm is restated sequentially in oracle/mpcqp_cpu.c -- see DESIGN.md.
 #include "mpcqp_build.h"
+
+#include <chrono>
 #ifdef MPCQP_ONLY_N
 #include "mpcqp_solve.h"  // development builds: one horizon, one translation unit
 #endif
@@ -99,6 +101,18 @@ const mpcqp::fleet_loop_t kFleetLoops[MPCQP_WIDE_MIN_HORIZON] = {
     MPCQP_F(24), MPCQP_F(25), MPCQP_F(26), MPCQP_F(27), MPCQP_F(28), MPCQP_F(29), MPCQP_F(30), MPCQP_F(31),
     MPCQP_F(32)};
 #undef MPCQP_F
+#ifdef MPCQP_ONLY_N
+#define MPCQP_S(N) ((N) == MPCQP_ONLY_N ? &mpcqp::launch_serve<MPCQP_ONLY_N> : nullptr)
+#else
+#define MPCQP_S(N) &mpcqp::launch_serve<N>
+#endif
+const mpcqp::serve_t kServers[MPCQP_WIDE_MIN_HORIZON] = {
+    nullptr,     MPCQP_S(1),  MPCQP_S(2),  MPCQP_S(3),  MPCQP_S(4),  MPCQP_S(5),  MPCQP_S(6),  MPCQP_S(7),
+    MPCQP_S(8),  MPCQP_S(9),  MPCQP_S(10), MPCQP_S(11), MPCQP_S(12), MPCQP_S(13), MPCQP_S(14), MPCQP_S(15),
+    MPCQP_S(16), MPCQP_S(17), MPCQP_S(18), MPCQP_S(19), MPCQP_S(20), MPCQP_S(21), MPCQP_S(22), MPCQP_S(23),
+    MPCQP_S(24), MPCQP_S(25), MPCQP_S(26), MPCQP_S(27), MPCQP_S(28), MPCQP_S(29), MPCQP_S(30), MPCQP_S(31),
+    MPCQP_S(32)};
+#undef MPCQP_S
 
 // per-QP doubles of the solver state buffer (debug state of the one-wave kernel, the workspace
 // of the long-horizon kernel)
@@ -173,6 +187,10 @@ int ensure_buffers(mpcqp_ws* ws, bool model, bool state, hipStream_t s) {
   if (e != hipSuccess) return fail(MPCQP_E_HIP, std::string("hipMalloc (workspace buffers): ") + hipGetErrorString(e));
   return MPCQP_OK;
 }
+serve_t server(const mpcqp_params& p) {
+  if (wide_solve(p) || p.debug_state || p.horizon < 1 || p.horizon >= MPCQP_WIDE_MIN_HORIZON) return nullptr;
+  return kServers[p.horizon];
+}
 fleet_loop_t fleet_looper(const mpcqp_params& p) {
   if (wide_solve(p) || p.debug_state || p.horizon < 1 || p.horizon >= MPCQP_WIDE_MIN_HORIZON) return nullptr;
   return kFleetLoops[p.horizon];
@@ -211,6 +229,9 @@ int mpcqp_create(const mpcqp_params* p, int max_batch, int device, mpcqp_ws** ws
   w->stage_in = w->stage_in_d = nullptr;
   w->stage_out = w->stage_out_d = nullptr;
   w->stage_stream = nullptr;
+  w->serve_box = w->serve_box_d = nullptr;
+  w->serve_seq = 0;
+  w->serve_live = false;
   e = hipMalloc(&w->dparams, 2 * sizeof(mpcqp_params));
   if (e == hipSuccess) e = hipMalloc(&w->dorder, sizeof(int32_t) * (size_t)max_batch);
   if (e != hipSuccess) {
@@ -228,10 +249,13 @@ int mpcqp_create(const mpcqp_params* p, int max_batch, int device, mpcqp_ws** ws
   return MPCQP_OK;
 }
 
+static void serve_stop(mpcqp_ws* ws);
+
 int mpcqp_set_params(mpcqp_ws* ws, const mpcqp_params* p) {
   if (!ws) return fail(MPCQP_E_ARG, "null ws");
   int rc = check_params(p);
   if (rc) return rc;
+  serve_stop(ws);  // a running B = 1 server holds the old parameter block
   if (p->horizon != ws->p.horizon) return fail(MPCQP_E_HORIZON, "set_params cannot change the horizon");
   if (p->reproducible != ws->p.reproducible) return fail(MPCQP_E_ARG, "set_params cannot change reproducible");
   ws->p = *p;
@@ -250,7 +274,9 @@ void mpcqp_destroy(mpcqp_ws* ws) {
   (void)hipFree(ws->state);
   (void)hipFree(ws->dparams);
   (void)hipFree(ws->dorder);
+  serve_stop(ws);
   if (ws->stage_stream) (void)hipStreamSynchronize(ws->stage_stream);
+  if (ws->serve_box) (void)hipHostFree(ws->serve_box);
   if (ws->stage_in) (void)hipHostFree(ws->stage_in);
   if (ws->stage_out) (void)hipHostFree(ws->stage_out);
   if (ws->stage_stream) (void)hipStreamDestroy(ws->stage_stream);
@@ -369,6 +395,96 @@ int mpcqp_solve_staged(mpcqp_ws* ws) {
   if (rc) return rc;
   const hipError_t e = hipStreamSynchronize(s);
   if (e != hipSuccess) return fail(MPCQP_E_DEVICE, std::string("hipStreamSynchronize: ") + hipGetErrorString(e));
+  return MPCQP_OK;
+}
+
+// The B = 1 server (k_serve): ends a live server wave (kServeStop) and waits for it.
+static void serve_stop(mpcqp_ws* ws) {
+  if (!ws || !ws->serve_live) return;
+  auto* box = static_cast<mpcqp::ServeBox*>(ws->serve_box);
+  __atomic_store_n(&box->req, mpcqp::kServeStop, __ATOMIC_RELEASE);
+  (void)hipStreamSynchronize(ws->stage_stream);
+  // the next request continues the sequence after the last completed one
+  __atomic_store_n(&box->req, __atomic_load_n(&box->done, __ATOMIC_ACQUIRE), __ATOMIC_RELEASE);
+  ws->serve_seq = __atomic_load_n(&box->done, __ATOMIC_ACQUIRE);
+  ws->serve_live = false;
+}
+
+int mpcqp_solve_served(mpcqp_ws* ws) {
+  if (!ws) return fail(MPCQP_E_ARG, "null ws");
+  if (!ws->stage_in) return fail(MPCQP_E_STATE, "mpcqp_solve_served before mpcqp_stage");
+  const mpcqp::serve_t launch = mpcqp::server(ws->p);
+  if (!launch) return mpcqp_solve_staged(ws);  // long horizons, reproducible or debug builds
+  if (!ws->serve_box) {
+    int cur = -1;
+    hipError_t e = hipGetDevice(&cur);
+    if (e == hipSuccess && cur != ws->device) e = hipSetDevice(ws->device);
+    void* box = nullptr;
+    void* dbox = nullptr;
+    if (e == hipSuccess) e = hipHostMalloc(&box, sizeof(mpcqp::ServeBox), hipHostMallocMapped | hipHostMallocCoherent);
+    if (e == hipSuccess) e = hipHostGetDevicePointer(&dbox, box, 0);
+    if (cur >= 0 && cur != ws->device) (void)hipSetDevice(cur);
+    if (e != hipSuccess) {
+      if (box) (void)hipHostFree(box);
+      return fail(MPCQP_E_HIP, std::string("B=1 server mailbox: ") + hipGetErrorString(e));
+    }
+    std::memset(box, 0, sizeof(mpcqp::ServeBox));
+    ws->serve_box = box;
+    ws->serve_box_d = dbox;
+    ws->serve_seq = 0;
+  }
+  auto* box = static_cast<mpcqp::ServeBox*>(ws->serve_box);
+  uint32_t seq = ws->serve_seq + 1;
+  if (seq == mpcqp::kServeStop) seq = 1;
+  ws->serve_seq = seq;
+  __atomic_store_n(&box->req, seq, __ATOMIC_RELEASE);  // after the caller's input writes (x86: ordered)
+  auto relaunch = [&]() -> int {
+    int32_t off[7];
+    stage_offsets(ws->p.horizon, off);
+    mpcqp::ServeLaunch L{};
+    L.box = static_cast<mpcqp::ServeBox*>(ws->serve_box_d);
+    L.in = ws->stage_in_d;
+    L.out = ws->stage_out_d;
+    for (int i = 0; i < 6; ++i) L.off[i] = off[i];
+    L.idle_ticks = 200000;  // 2 ms at 100 MHz
+    launch(ws->stage_stream, ws->p, L);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return fail(MPCQP_E_HIP, std::string("k_serve launch: ") + hipGetErrorString(e));
+    ws->serve_live = true;
+    return MPCQP_OK;
+  };
+  // the wave leaves 2 ms after its last request: past 1.5 ms, look before trusting it is there
+  const auto now = std::chrono::steady_clock::now();
+  if (ws->serve_live && now - ws->serve_last > std::chrono::microseconds(1500) &&
+      hipStreamQuery(ws->stage_stream) == hipSuccess)
+    ws->serve_live = false;
+  if (!ws->serve_live) {
+    const int rc = relaunch();
+    if (rc) return rc;
+  }
+  // wait for done == seq; every ~20 us of waiting, look whether the wave left (idle timeout racing
+  // this request, or a fault) and relaunch it
+  long spins = 0;
+  const auto t_start = now;
+  while (__atomic_load_n(&box->done, __ATOMIC_ACQUIRE) != seq) {
+    __builtin_ia32_pause();
+    if (++spins % 2048 == 0) {
+      const hipError_t q = hipStreamQuery(ws->stage_stream);
+      if (q == hipSuccess) {  // the wave has exited
+        if (__atomic_load_n(&box->done, __ATOMIC_ACQUIRE) == seq) break;
+        ws->serve_live = false;
+        const int rc = relaunch();
+        if (rc) return rc;
+      } else if (q != hipErrorNotReady) {
+        ws->serve_live = false;
+        return fail(MPCQP_E_DEVICE, std::string("B=1 server: ") + hipGetErrorString(q));
+      }
+      if (std::chrono::steady_clock::now() - t_start > std::chrono::seconds(30)) {
+        return fail(MPCQP_E_DEVICE, "B=1 server: no answer within 30 s");
+      }
+    }
+  }
+  ws->serve_last = std::chrono::steady_clock::now();
   return MPCQP_OK;
 }
 

@@ -3,6 +3,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <chrono>
 #include <cmath>
 #include <cstdint>
 #include <cstdio>
@@ -298,6 +299,28 @@ struct LoopTrigger {
 };
 template <int N>
 void launch_fleet_loop(hipStream_t s, const mpcqp_params* P, const mpcqp_fleet& f, int steps, const LoopTrigger& tr);
+// The B = 1 server (mpcqp_solve_served): one resident wave that solves the QP of the workspace's
+// staging block each time the host raises `req`, then publishes `done`.  In pinned, mapped,
+// coherent host memory; req and done on separate 64-byte lines.
+struct ServeBox {
+  uint32_t req;
+  uint32_t pad0[15];
+  uint32_t done;
+  uint32_t pad1[15];
+};
+constexpr uint32_t kServeStop = 0xffffffffu;  // req value that ends the server
+struct ServeLaunch {
+  ServeBox* box;      // device address of the mailbox
+  const double* in;   // device address of the staging input block (x0 | ref | u_prev)
+  uint8_t* out;       // device address of the staging output block
+  int32_t off[6];     // output block offsets (u0, X, U, status, iters, active)
+  uint64_t idle_ticks;  // s_memrealtime ticks (100 MHz) without a request after which the wave exits
+};
+template <int N>
+void launch_serve(hipStream_t s, const mpcqp_params& p, const ServeLaunch& L);
+typedef void (*serve_t)(hipStream_t, const mpcqp_params&, const ServeLaunch&);
+// nullptr when the parameter block does not run the one-wave kernel; defined in mpcqp.hip
+serve_t server(const mpcqp_params& p);
 typedef void (*fleet_loop_t)(hipStream_t, const mpcqp_params*, const mpcqp_fleet&, int, const LoopTrigger&);
 // nullptr when the parameter block does not run the one-wave kernel; defined in mpcqp.hip
 fleet_loop_t fleet_looper(const mpcqp_params& p);
@@ -347,6 +370,12 @@ struct mpcqp_ws {
   uint8_t* stage_out;    // host address (u0 | X | U | status | iters | active)
   uint8_t* stage_out_d;  // its device address
   hipStream_t stage_stream;
+  // the B = 1 server: mailbox (host / device address), sequence number, a server kernel enqueued
+  void* serve_box;
+  void* serve_box_d;
+  uint32_t serve_seq;
+  bool serve_live;
+  std::chrono::steady_clock::time_point serve_last;  // the last completed request (host clock)
 };
 
 namespace mpcqp {

@@ -414,6 +414,15 @@ struct FleetWin {
   __device__ __forceinline__ double upv(int i) const { return u[i]; }
 };
 
+// ServeWin: the B = 1 server (k_serve): the caller's buffers like BatchWin, with the lane index made
+// opaque per solve (otherwise LICM hoists every lane-derived value of the solver out of the serve loop
+// and holds it across requests).
+struct ServeWin {
+  static constexpr bool kFleet = false;
+  int ln;
+  __device__ __forceinline__ int lane() const { return ln; }
+};
+
 // ------------------------------------------------------------------ K2 phase 1: setup
 // Condensing (states and slacks eliminated) + OSQP Ruiz/cost scaling.  Leaves the scaled
 // problem on chip for the later phases: Pbar (symmetric, row-major) in the solve LDS, the
@@ -1789,9 +1798,54 @@ __global__ __launch_bounds__(kWave, kSolveWavesPerEU<N>) void k_fleet_loop(const
   }
 }
 
+// ------------------------------------------------------------------ B = 1 server
+// One resident wave serving the sequential closed loop of TrajectoryTracker.track: it waits for the
+// host to raise box->req (system-scope loads of pinned host memory, s_sleep between polls), solves the
+// one QP of the staging input block with solve_one (the k_solve driver), writes the outputs into the
+// staging output block, releases them at system scope and publishes box->done = req.  No launch and no
+// stream synchronisation per step.  Exit conditions every path reaches: req == kServeStop, or no new
+// request within idle_ticks of s_memrealtime (the host relaunches the wave at its next request).
+template <int N>
+__global__ __launch_bounds__(kWave, 1) void k_serve(mpcqp_params p, mpcqp::ServeLaunch L) {  // one resident wave: the whole register file
+  __shared__ SolveLds<N> sm;
+  const int lane = threadIdx.x;
+  uint32_t last = __builtin_amdgcn_readfirstlane(
+      __hip_atomic_load(&L.box->done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
+  for (;;) {
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    uint32_t req = last;
+    while (req == last) {
+      req = __builtin_amdgcn_readfirstlane(
+          __hip_atomic_load(&L.box->req, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
+      if (req != last) break;
+      if (__builtin_amdgcn_s_memrealtime() - t0 > L.idle_ticks) return;  // idle: leave, the host relaunches
+      __builtin_amdgcn_s_sleep(1);
+    }
+    if (req == mpcqp::kServeStop) return;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // system scope: the inputs the host wrote before req
+    int ln = lane;  // opaque per solve (ServeWin)
+    asm volatile("" : "+v"(ln));
+    const double* in = L.in;
+    uint8_t* o = L.out;
+    double Ul;
+    solve_one<N>(p, 0, nullptr, in, in + 4, in + 4 + 4 * (N + 1), ServeWin{ln}, sm,
+                 reinterpret_cast<double*>(o + L.off[0]), reinterpret_cast<double*>(o + L.off[1]),
+                 reinterpret_cast<double*>(o + L.off[2]), reinterpret_cast<int32_t*>(o + L.off[3]),
+                 reinterpret_cast<int32_t*>(o + L.off[4]), o + L.off[5], Ul);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // system scope: the outputs before done
+    if (lane == 0) __hip_atomic_store(&L.box->done, req, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    last = req;
+    __syncthreads();  // the next solve reuses the LDS
+  }
+}
+
 }  // namespace
 
 namespace mpcqp {
+template <int N>
+void launch_serve(hipStream_t s, const mpcqp_params& p, const ServeLaunch& L) {
+  hipLaunchKernelGGL(k_serve<N>, dim3(1), dim3(kWave), 0, s, p, L);
+}
 template <int N>
 void launch_solve(hipStream_t s, const Launch& L) {
   hipLaunchKernelGGL(k_solve<N>, dim3(L.B), dim3(kWave), 0, s, *L.p, L.B, L.mask, L.model, L.x0, L.ref, L.u_prev,

@@ -269,6 +269,7 @@ _SYMBOLS = {
     "mpcqp_stage": ([ctypes.c_void_p, ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_void_p),
                      ctypes.POINTER(ctypes.c_int32)], ctypes.c_int),
     "mpcqp_solve_staged": ([ctypes.c_void_p], ctypes.c_int),
+    "mpcqp_solve_served": ([ctypes.c_void_p], ctypes.c_int),
 }
 
 

@@ -12,6 +12,7 @@ from __future__ import annotations
 
 import ctypes
 import logging
+import os
 from collections import OrderedDict
 from dataclasses import dataclass
 from typing import NamedTuple, Optional, Tuple
@@ -175,8 +176,9 @@ class BatchedMPCController:
         """One QP for the sequential closed loop of ``TrajectoryTracker.track``, where host overhead
         dominates a B=1 step.  The workspace's own blocks of pinned, device-mapped host memory hold
         the inputs and outputs, which the kernels read and write in place (``mpcqp_stage`` /
-        ``mpcqp_solve_staged``, include/mpcqp.h): the inputs are written into the block, then ONE
-        library call launches the solve on the workspace's private stream and waits for it.
+        ``mpcqp_solve_served``, include/mpcqp.h): the inputs are written into the block, then ONE
+        library call hands the QP to the workspace's resident solver wave (started by the first
+        call, gone after 2 ms idle) and waits for its answer -- no kernel launch per step.
         ``x0`` (4,), ``ref`` (>= N+1, 4) -- rows 0..N are used --, ``u_prev`` (2,) host arrays.
         Returns host numpy ``(status, u0, X, U)``; X (4, N+1) and U (2, N) are fresh arrays.
         A fault that surfaces at the synchronisation raises ``_lib.DeviceError``."""
@@ -189,12 +191,12 @@ class BatchedMPCController:
             io["up"][:] = 0.0
         else:
             io["up"][:] = u_prev
-        rc = self._L.mpcqp_solve_staged(self._ws)
+        rc = self._solve1(self._ws)
         if rc != 0:
             msg = self._L.mpcqp_last_error().decode(errors="replace")
             if rc == _lib.E_DEVICE:
-                raise _lib.DeviceError(f"mpcqp_solve_staged: {msg}")
-            raise _lib.LibraryError(f"mpcqp_solve_staged failed ({rc}): {msg}")
+                raise _lib.DeviceError(f"B=1 solve: {msg}")
+            raise _lib.LibraryError(f"B=1 solve failed ({rc}): {msg}")
         return int(io["status"][0]), io["u0"].copy(), io["X"].copy(), io["U"].copy()
 
     _one = None
@@ -203,6 +205,10 @@ class BatchedMPCController:
         """numpy views of the workspace's B=1 staging blocks (allocated by the first mpcqp_stage;
         an allocation failure raises DeviceError)."""
         N = self.horizon
+        # the resident B=1 server (mpcqp_solve_served: no launch per call) unless MPCQP_B1_SERVER=0
+        # asks for a launch per call (mpcqp_solve_staged)
+        self._solve1 = (self._L.mpcqp_solve_staged if os.environ.get("MPCQP_B1_SERVER", "1") == "0"
+                        else self._L.mpcqp_solve_served)
         hin, hout = ctypes.c_void_p(), ctypes.c_void_p()
         offs = (ctypes.c_int32 * 6)()
         with self._torch.cuda.device(self.device):

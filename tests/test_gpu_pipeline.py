@@ -192,3 +192,35 @@ def test_drop_in_unpolished_result_is_osqp_scaled(cuda):
                 assert Uq is not None and np.array_equal(Uq, exp_U), q
             else:
                 assert Uq is None, q
+
+
+def test_b1_server_matches_launch_per_call(cuda, monkeypatch):
+    """The resident B=1 server (mpcqp_solve_served) returns exactly what a launch per call
+    (mpcqp_solve_staged) returns, across its idle exit (no request for > 2 ms: the next call starts
+    the wave again), a parameter change (set_params stops it) and back-to-back requests."""
+    import time
+
+    from mpcqp import scenarios
+    from mpcqp.config import MPCConfig
+    from mpcqp.control.mpc_controller import BatchedMPCController
+
+    b = scenarios.config3(12, horizon=15, seed=41)
+    params = MPCConfig(horizon=15).to_parameters(0.8)
+    res = {}
+    for mode in ("0", "1"):
+        monkeypatch.setenv("MPCQP_B1_SERVER", mode)
+        ctrl = BatchedMPCController(params, 1, device="cuda:0")
+        out = []
+        for q in range(12):
+            if q in (4, 9):
+                time.sleep(0.01)  # past the server's 2 ms idle limit
+            if q == 7:
+                ctrl.set_params(params)  # stops a live server
+            out.append(ctrl.solve_one(b.x0[q], b.ref[q], b.u_prev[q]))
+        ctrl.close()
+        res[mode] = out
+    for q in range(12):
+        a, c = res["0"][q], res["1"][q]
+        assert a[0] == c[0] == 1
+        for x, y in zip(a[1:], c[1:]):
+            assert np.array_equal(x, y), q
