@@ -454,9 +454,12 @@ def config1_closed_loop() -> dict:
         "cpu_ms_per_step_default_schedule": 1e3 * cpu_default_s / max(1, len(c_default_states)),
         "max_state_diff_px": dev,
         "polish_schedule": sched,
+        "b1_path": "launch" if os.environ.get("MPCQP_B1_SERVER", "1") == "0" else "served",
         "note": "each leg the best of three runs after a warm one, all with the B=1 drop-in's latency "
                 "polish schedule (polish_schedule; the batch default is tuned for a batch's slowest QP); "
-                "gpu_ms_per_step: the drop-in TrajectoryTracker loop, one B=1 launch + host sync per step; "
+                "gpu_ms_per_step: the drop-in TrajectoryTracker loop, one B=1 solve per step (b1_path: "
+                "'served' = a request to the resident server wave, mpcqp_solve_served, the default; "
+                "'launch' = one kernel launch + stream sync per solve, MPCQP_B1_SERVER=0); "
                 "gpu_device_loop_ms_per_step: the same loop as one vehicle of the fused device loop "
                 "(mpcqp_fleet_loop: one launch for the run, launch to results on the host; the "
                 "reference build and fleet buffer setup are gpu_device_loop_setup_s)",
@@ -595,6 +598,59 @@ def osqp_settings_leg(params, x0, ref, u_prev, steps: int, warmup: int, device, 
         ctrl.close()
 
 
+def pipelined_leg(params, x0, ref, u_prev, steps: int, warmup: int, device, method: str, extra: dict,
+                  U_ref, streams: int = 2) -> dict:
+    """The headline batch solved `steps` times with step k on stream k % `streams` (each stream its own
+    workspace and outputs), so one batch's dispatch tail -- its slowest QPs, DESIGN.md §5 -- overlaps
+    the next batch's start.  Reported beside `value`, never as it: every step is still one whole batch
+    with its own build and solve, but `streams` batches may be in flight (a serving front end with
+    independent requests; a closed loop whose next batch needs this one's u0 cannot do this)."""
+    import torch
+
+    from mpcqp import _lib
+    from mpcqp.control.mpc_controller import BatchedMPCController
+
+    B = len(x0)
+    ctrls = [BatchedMPCController(params, max(1, B), device=device, method=method, **extra) for _ in range(streams)]
+    try:
+        x0_t, ref_t, up_t = (torch.from_numpy(a).to(device) for a in (x0, ref, u_prev))
+        L = _lib.lib()
+        strs = [torch.cuda.Stream(device) for _ in range(streams)]
+        cur = torch.cuda.current_stream(device)
+        for st in strs:  # the inputs were written on the current stream
+            st.wait_stream(cur)
+
+        issued = [0]  # warmup steps rotate over the streams too
+
+        def step(k: int) -> None:
+            j = issued[0] % streams
+            issued[0] += 1
+            c, st = ctrls[j], strs[j]
+            s = ctypes.c_void_p(st.cuda_stream)
+            _lib.check(L.mpcqp_build(c._ws, B, x0_t.data_ptr(), ref_t.data_ptr(), up_t.data_ptr(), s), "build")
+            _lib.check(L.mpcqp_solve(c._ws, B, c._u0.data_ptr(), c._X.data_ptr(), c._U.data_ptr(),
+                                     c._status.data_ptr(), c._iters.data_ptr(), c._active.data_ptr(), s), "solve")
+
+        elapsed = timed_steps(step, steps, max(warmup, streams), DistContext(),
+                              lambda: torch.cuda.synchronize(device))
+        solved = float((ctrls[0]._status[:B] == 1).sum().item())
+        same = all(torch.equal(c._U[:B], U_ref) for c in ctrls)
+        return {
+            "value": solved * steps / elapsed,
+            "unit": "QP/s",
+            "streams": streams,
+            "ms_per_step": 1e3 * elapsed / steps,
+            "identical_to_headline": bool(same),
+            "note": f"the headline batch, step k on stream k % {streams}: consecutive batches overlap, so one "
+                    "batch's slowest QPs share the GPU with the next batch's start; same timing rule as "
+                    "the headline line (K steps between synchronizations); not the headline value, "
+                    "which runs one batch at a time",
+        }
+    finally:
+        for c in ctrls:
+            c.close()
+
+
 # ------------------------------------------------------------------ main
 def main() -> int:
     ap = argparse.ArgumentParser()
@@ -617,6 +673,8 @@ def main() -> int:
     ap.add_argument("--check-sample", type=int, default=512, help="QPs of the gathered result rank 0 checks")
     ap.add_argument("--no-config1", action="store_true", help="skip the config-1 closed-loop line")
     ap.add_argument("--no-config5", action="store_true", help="skip the config-5 swarm line")
+    ap.add_argument("--no-pipelined", action="store_true",
+                    help="skip the leg that overlaps consecutive batches on two streams")
     ap.add_argument("--no-osqp-settings", action="store_true",
                     help="skip the leg that reruns the batch under OSQP's own scaling / polish defaults")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
@@ -771,6 +829,9 @@ def main() -> int:
                                         g["status"], idx, g["iters"], settings=extra)
             out["rel_err"]["gathered_qps"] = int(len(g["status"]))
             out["rel_err"]["gathered_solved"] = int((g["status"] == 1).sum())
+        if world == 1 and not args.no_pipelined:
+            out["pipelined"] = pipelined_leg(params, x0, ref, u_prev, args.steps, args.warmup, device, args.method,
+                                             extra, ctrl._U[:B])
         if world == 1 and not args.no_osqp_settings:
             out["osqp_settings"] = osqp_settings_leg(params, x0, ref, u_prev, args.steps, args.warmup, device,
                                                      args.method, extra, min(args.check_sample, 256))

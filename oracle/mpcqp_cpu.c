@@ -37,8 +37,9 @@
 
 #include "../include/mpcqp.h"
 
-/* static per-thread storage: the restatement stops at N = 127 (the GPU goes to MPCQP_MAX_HORIZON) */
-#define MAXN (MPCQP_MAX_HORIZON < 127 ? MPCQP_MAX_HORIZON : 127)
+/* static per-thread storage: the restatement stops at N = 130 (the GPU goes to MPCQP_MAX_HORIZON); a
+   row stride of 2 MAXN = 260 doubles, not a power of two, keeps column walks off one cache set */
+#define MAXN (MPCQP_MAX_HORIZON < 130 ? MPCQP_MAX_HORIZON : 130)
 #define MAXNV (2 * MAXN)
 #define MAXR (5 * MAXN)
 #define PI_D 3.141592653589793

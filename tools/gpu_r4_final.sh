@@ -1,0 +1,27 @@
+# Round 4 measurement set with the round's library: all GPU tests, smoke, the bench line, the
+# kernel-trace profile, PMC passes on the headline launch alone (no side legs, so the entry keys to
+# the headline settings), config 2 / config 4 lines, horizons 32 / 40 / 64 / 128.
+# usage: gpurun --timeout 1150 -- 'bash tools/gpu_r4_final.sh'
+set -o pipefail
+R=$GRAFT_REPO_ROOT; O=$R/gpurun_out; mkdir -p $O
+SIDE="--cpu-seconds 0 --no-config1 --no-config5 --no-osqp-settings --no-pipelined"
+timeout -k 10 400 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > $O/f_pytest_gpu.log 2>&1 &&
+timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > $O/f_smoke.log 2>&1 &&
+timeout -k 10 300 python bench.py > $O/f_bench.json 2> $O/f_bench.err &&
+cd /tmp && export TMPDIR=/tmp &&
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/f_prof -o run -f csv -- python3 $R/bench.py --steps 10 --warmup 2 --cpu-seconds 0 > $O/f_bench_prof.json 2> $O/f_bench_prof.err &&
+timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -d $O/pmc_fetch -o run -f csv -- python3 $R/bench.py --steps 3 --warmup 1 $SIDE > $O/pmc_fetch.log 2>&1 &&
+timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE -d $O/pmc_write -o run -f csv -- python3 $R/bench.py --steps 3 --warmup 1 $SIDE > $O/pmc_write.log 2>&1 &&
+timeout -s KILL 120 rocprofv3 --pmc TCC_EA0_RDREQ_sum TCC_EA0_WRREQ_sum -d $O/pmc_req -o run -f csv -- python3 $R/bench.py --steps 3 --warmup 1 $SIDE > $O/pmc_req.log 2>&1 &&
+timeout -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU -d $O/pmc_sq -o run -f csv -- python3 $R/bench.py --steps 3 --warmup 1 $SIDE > $O/pmc_sq.log 2>&1 &&
+timeout -s KILL 120 rocprofv3 --pmc SQ_INSTS_VALU_FLOPS_FP64 SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_TRANS_F64 SQ_INSTS_SALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT -d $O/pmc_f64 -o run -f csv -- python3 $R/bench.py --steps 3 --warmup 1 $SIDE > $O/pmc_f64.log 2>&1 &&
+cd $R &&
+timeout -k 10 200 python bench.py --config config2 --cpu-seconds 0 --no-config1 > $O/f_c2.json 2> $O/f_c2.err &&
+timeout -k 10 200 python bench.py --config config4 --batch 2048 --cpu-seconds 0 --no-config1 > $O/f_c4_b2048.json 2> $O/f_c4.err &&
+timeout -k 10 200 python bench.py --config config4 --batch 4096 --cpu-seconds 0 --no-config1 > $O/f_c4_b4096.json 2>> $O/f_c4.err &&
+timeout -k 10 200 python bench.py --config config4 --cpu-seconds 0 --no-config1 > $O/f_c4_b16384.json 2>> $O/f_c4.err &&
+timeout -k 10 200 python bench.py --horizon 32 --steps 10 --warmup 2 --cpu-seconds 0 --no-config1 --no-osqp-settings --check-sample 128 > $O/f_N32.json 2> $O/f_N32.err &&
+timeout -k 10 200 python bench.py --horizon 40 --steps 10 --warmup 2 --cpu-seconds 0 --no-config1 --no-osqp-settings --check-sample 128 > $O/f_N40.json 2> $O/f_N40.err &&
+timeout -k 10 200 python bench.py --horizon 64 --steps 3 --warmup 1 --cpu-seconds 0 --no-config1 --no-osqp-settings --no-pipelined --check-sample 32 > $O/f_N64.json 2> $O/f_N64.err &&
+timeout -k 10 300 python bench.py --horizon 128 --batch 1024 --steps 2 --warmup 1 --cpu-seconds 0 --no-config1 --no-osqp-settings --no-pipelined --check-sample 8 > $O/f_N128.json 2> $O/f_N128.err
+rc=$?; echo "exit $rc"; tail -3 $O/f_pytest_gpu.log; exit $rc
