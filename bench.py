@@ -667,6 +667,8 @@ def main() -> int:
                     help="ADMM iteration of the first early polish attempt (default: the library's; 0 = off)")
     ap.add_argument("--polish-near", type=float, default=None,
                     help="residual/tolerance ratio that triggers an early polish (default: the library's; 0 = off)")
+    ap.add_argument("--pairing", default="auto", choices=["auto", "on", "off"],
+                    help="two QPs per wave for N <= 15 (mpcqp_set_pairing; the same results bit for bit)")
     ap.add_argument("--set", action="append", default=[], metavar="KEY=VALUE",
                     help="development: override a solver setting of mpcqp_params (repeatable)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline sample length (0 = skip)")
@@ -707,7 +709,7 @@ def main() -> int:
     for kv in args.set:
         k, v = kv.split("=", 1)
         extra[k] = float(v) if "." in v or "e" in v else int(v)
-    ctrl = BatchedMPCController(params, max(1, B), device=device, method=args.method, **extra)
+    ctrl = BatchedMPCController(params, max(1, B), device=device, method=args.method, pairing=args.pairing, **extra)
     x0_t = torch.from_numpy(x0).to(device)
     ref_t = torch.from_numpy(ref).to(device)
     up_t = torch.from_numpy(u_prev).to(device)
@@ -789,6 +791,7 @@ def main() -> int:
                 "nu": 2,
                 "method": method_label(ctrl._cparams),
                 "solver_settings": solver_settings(ctrl._cparams),
+                "pairing": args.pairing,
                 "parallelism": f"dp{world} (independent contiguous shards, {'strong' if strong else 'weak'})",
             },
             "solved_fraction": solved_all / total,

@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define MPCQP_ABI_VERSION 7
+#define MPCQP_ABI_VERSION 8
 
 /* error codes (function return values) */
 #define MPCQP_OK 0
@@ -200,6 +200,18 @@ int mpcqp_solve_staged(mpcqp_ws* ws);
  * waits for it to go idle.  Horizons without the one-wave kernel (N > 32, reproducible, debug
  * builds) run mpcqp_solve_staged. */
 int mpcqp_solve_served(mpcqp_ws* ws);
+
+/* Two QPs per wave for horizons N <= 15 (2N <= 30 variables: a one-wave QP leaves half its lanes on
+ * padding): lanes 0-31 and 32-63 of a wave solve two QPs of the batch (mpcqp_solve with the model
+ * built in the solve) or two vehicles of the fused loop (mpcqp_fleet_loop, mpcqp_swarm_loop), with
+ * the results of the one-QP-per-wave kernel bit for bit.  MPCQP_PAIR_AUTO (the default) pairs once
+ * a launch has more QPs than the device has wave slots (8 per CU); ON / OFF force it.  Ignored where
+ * the one-wave kernel does not run (N > 15, reproducible, debug_state).  No counterpart in the
+ * reference (OSQP solves one QP per call). */
+#define MPCQP_PAIR_OFF 0
+#define MPCQP_PAIR_ON 1
+#define MPCQP_PAIR_AUTO 2
+int mpcqp_set_pairing(mpcqp_ws* ws, int mode);
 
 /*
  * Closed-loop fleet: V vehicles tracking their own references, one MPC step each per call

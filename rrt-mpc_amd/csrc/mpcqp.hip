@@ -102,6 +102,16 @@ const mpcqp::fleet_loop_t kFleetLoops[MPCQP_WIDE_MIN_HORIZON] = {
     MPCQP_F(32)};
 #undef MPCQP_F
 #ifdef MPCQP_ONLY_N
+#define MPCQP_P(N) ((N) == MPCQP_ONLY_N ? &mpcqp::launch_solve_pair<MPCQP_ONLY_N> : nullptr)
+#else
+#define MPCQP_P(N) &mpcqp::launch_solve_pair<N>
+#endif
+constexpr int kPairMaxHorizon = 15;  // n = 2N <= 30: two QPs per wave
+const mpcqp::pair_launcher_t kPairLaunchers[kPairMaxHorizon + 1] = {
+    nullptr,    MPCQP_P(1),  MPCQP_P(2),  MPCQP_P(3),  MPCQP_P(4),  MPCQP_P(5),  MPCQP_P(6),  MPCQP_P(7),
+    MPCQP_P(8), MPCQP_P(9),  MPCQP_P(10), MPCQP_P(11), MPCQP_P(12), MPCQP_P(13), MPCQP_P(14), MPCQP_P(15)};
+#undef MPCQP_P
+#ifdef MPCQP_ONLY_N
 #define MPCQP_S(N) ((N) == MPCQP_ONLY_N ? &mpcqp::launch_serve<MPCQP_ONLY_N> : nullptr)
 #else
 #define MPCQP_S(N) &mpcqp::launch_serve<N>
@@ -191,6 +201,18 @@ serve_t server(const mpcqp_params& p) {
   if (wide_solve(p) || p.debug_state || p.horizon < 1 || p.horizon >= MPCQP_WIDE_MIN_HORIZON) return nullptr;
   return kServers[p.horizon];
 }
+bool use_pairs(const mpcqp_ws* ws, int count) {
+  const mpcqp_params& p = ws->p;
+  if (wide_solve(p) || p.debug_state || p.horizon < 1 || p.horizon > kPairMaxHorizon || !kPairLaunchers[p.horizon])
+    return false;
+  if (ws->pairing == MPCQP_PAIR_ON) return true;
+  if (ws->pairing == MPCQP_PAIR_OFF) return false;
+  // auto: once the QPs outnumber the wave slots (2 per SIMD): below that every QP has a wave of its
+  // own, and pairing would only make each wave wait for the slower of its two QPs
+  int cus = 0;
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ws->device) != hipSuccess) cus = 0;
+  return cus > 0 && count > 8 * cus;
+}
 fleet_loop_t fleet_looper(const mpcqp_params& p) {
   if (wide_solve(p) || p.debug_state || p.horizon < 1 || p.horizon >= MPCQP_WIDE_MIN_HORIZON) return nullptr;
   return kFleetLoops[p.horizon];
@@ -232,6 +254,7 @@ int mpcqp_create(const mpcqp_params* p, int max_batch, int device, mpcqp_ws** ws
   w->serve_box = w->serve_box_d = nullptr;
   w->serve_seq = 0;
   w->serve_live = false;
+  w->pairing = MPCQP_PAIR_AUTO;
   e = hipMalloc(&w->dparams, 2 * sizeof(mpcqp_params));
   if (e == hipSuccess) e = hipMalloc(&w->dorder, sizeof(int32_t) * (size_t)max_batch);
   if (e != hipSuccess) {
@@ -283,6 +306,14 @@ void mpcqp_destroy(mpcqp_ws* ws) {
   delete ws;
 }
 
+int mpcqp_set_pairing(mpcqp_ws* ws, int mode) {
+  if (!ws) return fail(MPCQP_E_ARG, "null ws");
+  if (mode != MPCQP_PAIR_OFF && mode != MPCQP_PAIR_ON && mode != MPCQP_PAIR_AUTO)
+    return fail(MPCQP_E_ARG, "pairing mode must be MPCQP_PAIR_OFF, _ON or _AUTO");
+  ws->pairing = mode;
+  return MPCQP_OK;
+}
+
 int mpcqp_build(mpcqp_ws* ws, int B, const double* x0, const double* ref, const double* u_prev, void* stream) {
   if (!ws || !x0 || !ref) return fail(MPCQP_E_ARG, "null argument");
   if (B < 0 || B > ws->max_batch) return fail(MPCQP_E_BATCH, "batch exceeds workspace capacity");
@@ -319,7 +350,7 @@ int mpcqp_solve(mpcqp_ws* ws, int B, double* u0, double* X, double* U, int32_t* 
   L.x0 = ws->in_x0;
   L.ref = ws->in_ref;
   L.u_prev = ws->in_up;
-  mpcqp::launcher(ws->p)(s, L);
+  if (!(L.ref && mpcqp::use_pairs(ws, B) && kPairLaunchers[ws->p.horizon](s, L))) mpcqp::launcher(ws->p)(s, L);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return fail(MPCQP_E_HIP, std::string("k_solve launch: ") + hipGetErrorString(e));
   return MPCQP_OK;

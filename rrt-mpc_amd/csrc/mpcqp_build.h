@@ -14,8 +14,10 @@ struct LaneModel {
 // One wave per QP, lane k <= N holding window row k's yaw and speed: np.unwrap of the yaw
 // (mpc_controller.py:59-60), then linearize() at ref[max(k-1,0)], u = 0 (mpc_controller.py:65-70,
 // 108; vehicle_model.py:24-45).  Every lane of the wave must call this (DPP reads inactive lanes
-// as zero).
+// as zero).  Pair: the QP owns one 32-lane half (Lanes<true>, lane = the lane within it).
+template <bool Pair = false>
 __device__ __forceinline__ LaneModel build_lane(const mpcqp_params& p, int lane, double ryaw, double rv) {
+  using LN = Lanes<Pair>;
   const int N = p.horizon;
   LaneModel m{};
   // np.unwrap: ddmod = mod(dd + pi, 2pi) - pi; boundary fix; zero when |dd| < pi
@@ -31,9 +33,9 @@ __device__ __forceinline__ LaneModel build_lane(const mpcqp_params& p, int lane,
   // cumsum in numpy's sequential order (bit-exact).  Every correction is +0.0 or nonzero (ddmod -
   // dd of equal finite values is +0.0), so a window without a wrap sums to +0.0 throughout.
   double cs = 0.0, mine = 0.0;
-  if (wave_any(pc != 0.0))
+  if (LN::any(pc != 0.0))
     for (int j = 1; j <= N; ++j) {
-      cs = cs + readlane(pc, j);
+      cs = cs + LN::readv(pc, j);
       if (lane == j) mine = cs;
     }
   m.uyaw = lane == 0 ? ryaw : ryaw + mine;
@@ -61,10 +63,11 @@ __device__ __forceinline__ LaneModel build_lane(const mpcqp_params& p, int lane,
 // build_lane + the model block of one QP written to mb (global or LDS):
 // alpha[N] beta[N] gamma[N] eta[N] sigma[N] c0[N] c1[N] ref[(N+1)*4] x0[4] u_prev[2],
 // stride model_stride(N).  x0l = x0[lane] on lanes 0..3, upl = u_prev[lane-4] on lanes 4..5.
+template <bool Pair = false>
 __device__ __forceinline__ void build_qp(const mpcqp_params& p, int lane, double rx, double ry, double ryaw,
                                          double rv, double x0l, double upl, double* __restrict__ mb) {
   const int N = p.horizon;
-  const LaneModel m = build_lane(p, lane, ryaw, rv);
+  const LaneModel m = build_lane<Pair>(p, lane, ryaw, rv);
   if (lane <= N) {
     mb[7 * N + 4 * lane + 0] = rx;
     mb[7 * N + 4 * lane + 1] = ry;

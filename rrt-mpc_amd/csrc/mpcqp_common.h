@@ -194,6 +194,103 @@ template <int L>
 __device__ __forceinline__ void fmac_bc(double& acc, double w, double m) {
   asm("v_fmac_f64_dpp %0, %1, %2 row_newbcast:%3 row_mask:0xf bank_mask:0xf" : "+v"(acc) : "v"(w), "v"(m), "i"(L));
 }
+// ---- lane policies of the one-wave solver: a QP owns the whole wave (Lanes<false>, the layout
+// above) or one 32-lane half of it (Lanes<true>: two QPs per wave, lanes 0-31 and 32-63, for
+// n = 2N <= 30, where a whole-wave QP leaves lanes 30..63 computing on padding).  Every cross-lane
+// operation of a half stays inside it: 16-lane-row DPP, permlane16 swaps (rows 0<->1, 2<->3),
+// row_bcast:15 into rows 1 / 3, ds_bpermute within 32 lanes -- so the two QPs of a wave may take
+// different branches (the other half is masked off), and a half's sums and scans add the same
+// values in the same order as the whole-wave ones (lanes past n hold zeros in both layouts).
+template <bool Pair>
+struct Lanes;
+
+template <>
+struct Lanes<false> {
+  static constexpr int kLanes = kWave;
+  template <int NW>
+  __device__ __forceinline__ static void vbcast(double v, double w[4]) { bcast<NW>(v, w); }
+  template <int K>
+  __device__ __forceinline__ static double read(double v) { return readlane(v, K); }
+  __device__ __forceinline__ static double readv(double v, int l) { return readlane(v, l); }
+  __device__ __forceinline__ static int uniform(int l) { return __builtin_amdgcn_readfirstlane(l); }
+  __device__ __forceinline__ static double sum(double v) { return wave_sum(v); }
+  __device__ __forceinline__ static double max(double v) { return wave_max(v); }
+  __device__ __forceinline__ static bool any(bool b) { return wave_any(b); }
+  __device__ __forceinline__ static uint64_t ballot(bool b) { return __ballot(b); }
+  __device__ __forceinline__ static double shr2(double v) { return ::shr2(v); }
+  __device__ __forceinline__ static double shl2(double v) { return ::shl2(v); }
+  __device__ __forceinline__ static double shr4(double v) { return ::shr4(v); }
+  __device__ __forceinline__ static double shl4(double v) { return ::shl4(v); }
+  __device__ __forceinline__ static double shr1(double v) { return dpp<kWaveShr1>(v); }  // lane 0 <- 0
+  __device__ __forceinline__ static double scan(double v, int lane) { return scan_add(v, lane); }
+  __device__ __forceinline__ static double shfl(double v, int src) { return __shfl(v, src, kWave); }
+};
+
+// lane L of each 16-lane row, to the whole row (one v_mov_b32_dpp row_newbcast per word)
+template <int L>
+__device__ __forceinline__ double row_bc(double v) {
+  const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), 0x150 + L, 0xf, 0xf, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), 0x150 + L, 0xf, 0xf, false);
+  return __hiloint2double(hi, lo);
+}
+
+template <>
+struct Lanes<true> {
+  static constexpr int kLanes = 32;
+  __device__ __forceinline__ static int hl() { return (int)threadIdx.x & 31; }  // lane within the half
+  // w[c] lane l = v[16c + (l & 15)] of l's own half (c = 0, 1): one permlane16 swap per word
+  template <int NW>
+  __device__ __forceinline__ static void vbcast(double v, double w[4]) {
+    static_assert(NW <= 2, "a half holds 32 lanes");
+    const int lo = __double2loint(v), hi = __double2hiint(v);
+    const auto l16 = __builtin_amdgcn_permlane16_swap(lo, lo, false, false);  // rows {0,0,2,2} / {1,1,3,3}
+    const auto h16 = __builtin_amdgcn_permlane16_swap(hi, hi, false, false);
+    w[0] = __hiloint2double(h16[0], l16[0]);
+    w[1] = __hiloint2double(h16[1], l16[1]);
+    // DPP reads of a VGPR need two wait states after its VALU write; tie the pad to w
+    asm volatile("s_nop 1" : "+v"(w[0]), "+v"(w[1]));
+  }
+  template <int K>
+  __device__ __forceinline__ static double read(double v) {
+    double w[4];
+    vbcast<2>(v, w);
+    return row_bc<K % 16>(w[K / 16]);
+  }
+  __device__ __forceinline__ static double readv(double v, int l) { return __shfl(v, l, 32); }
+  __device__ __forceinline__ static int uniform(int l) { return l; }
+  // inclusive scan within the rows, then rows 1 / 3 take rows 0 / 2's total: lane 31 / 63 = the sum
+  __device__ __forceinline__ static double scan(double v, int lane) {
+    (void)lane;
+    v += dpp<kRowShr1>(v);
+    v += dpp<kRowShr2>(v);
+    v += dpp<kRowShr4>(v);
+    v += dpp<kRowShr8>(v);
+    v += dpp_rows<kRowBcast15, 0xa>(v);
+    return v;
+  }
+  __device__ __forceinline__ static double sum(double v) { return read<31>(scan(v, 0)); }
+  __device__ __forceinline__ static double max(double v) {  // v >= 0
+    v = max_nc(v, dpp<kRowShr1>(v));
+    v = max_nc(v, dpp<kRowShr2>(v));
+    v = max_nc(v, dpp<kRowShr4>(v));
+    v = max_nc(v, dpp<kRowShr8>(v));
+    v = max_nc(v, dpp_rows<kRowBcast15, 0xa>(v));
+    return read<31>(v);
+  }
+  __device__ __forceinline__ static uint64_t ballot(bool b) {
+    const uint64_t m = __ballot(b);
+    return (threadIdx.x & 32) ? (m >> 32) : (m & 0xffffffffull);
+  }
+  __device__ __forceinline__ static bool any(bool b) { return ballot(b) != 0ull; }
+  // wave shifts, cut at the half boundary (what crosses it reads as 0, as past the wave's ends)
+  __device__ __forceinline__ static double shr2(double v) { return hl() >= 2 ? ::shr2(v) : 0.0; }
+  __device__ __forceinline__ static double shl2(double v) { return hl() < 30 ? ::shl2(v) : 0.0; }
+  __device__ __forceinline__ static double shr4(double v) { return shr2(shr2(v)); }
+  __device__ __forceinline__ static double shl4(double v) { return shl2(shl2(v)); }
+  __device__ __forceinline__ static double shr1(double v) { return hl() >= 1 ? dpp<kWaveShr1>(v) : 0.0; }
+  __device__ __forceinline__ static double shfl(double v, int src) { return __shfl(v, src, 32); }
+};
+
 // compile-time loop: f(std::integral_constant<int, I>) for I in [B, E)
 template <int B, int E>
 struct Unroll {
@@ -278,6 +375,10 @@ struct Launch {
 };
 
 typedef void (*launcher_t)(hipStream_t, const Launch&);
+// two QPs per wave (k_solve_pair, N <= 15, fused K1); returns false where not instantiated
+typedef bool (*pair_launcher_t)(hipStream_t, const Launch&);
+template <int N>
+bool launch_solve_pair(hipStream_t s, const Launch& L);
 // K2a -> K2b -> K2c for horizon N; defined in mpcqp_solve.h, instantiated per horizon in
 // mpcqp_part.hip objects (parallel build) or in mpcqp.hip itself (MPCQP_ONLY_N dev builds).
 template <int N>
@@ -296,6 +397,7 @@ struct LoopTrigger {
   // reference first: a vehicle's step count follows its reference length, and the slowest
   // vehicles started last would set the run's tail once the vehicles outnumber the wave slots.
   const int32_t* order = nullptr;
+  bool pair = false;  // two vehicles per wave (N <= 15): k_fleet_loop<N, true>
 };
 template <int N>
 void launch_fleet_loop(hipStream_t s, const mpcqp_params* P, const mpcqp_fleet& f, int steps, const LoopTrigger& tr);
@@ -324,6 +426,8 @@ serve_t server(const mpcqp_params& p);
 typedef void (*fleet_loop_t)(hipStream_t, const mpcqp_params*, const mpcqp_fleet&, int, const LoopTrigger&);
 // nullptr when the parameter block does not run the one-wave kernel; defined in mpcqp.hip
 fleet_loop_t fleet_looper(const mpcqp_params& p);
+// k_solve_pair / k_fleet_loop<N, true> for `count` QPs or vehicles of this workspace's launch?
+bool use_pairs(const mpcqp_ws* ws, int count);
 // the long-horizon solve (N >= MPCQP_WIDE_MIN_HORIZON; mpcqp_wide.hip): one 256-thread workgroup
 // per QP, L.state = its workspace (wide_stride(N) doubles per QP)
 void launch_solve_wide(hipStream_t s, const Launch& L);
@@ -376,6 +480,8 @@ struct mpcqp_ws {
   uint32_t serve_seq;
   bool serve_live;
   std::chrono::steady_clock::time_point serve_last;  // the last completed request (host clock)
+  // two QPs per wave for N <= 15 (MPCQP_PAIR_*, mpcqp_set_pairing)
+  int pairing;
 };
 
 namespace mpcqp {

@@ -280,6 +280,7 @@ int enqueue_fleet_loop(mpcqp_ws* nominal, mpcqp_ws* relaxed, const mpcqp_fleet* 
     hipLaunchKernelGGL(k_fleet_order, dim3(1), dim3(kOrderBuckets), 0, s, *f, nominal->dorder);
     tro.order = nominal->dorder;
   }
+  tro.pair = mpcqp::use_pairs(nominal, f->vehicles);
   loop(s, nominal->dparams, *f, steps, tro);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return fail(MPCQP_E_HIP, std::string("k_fleet_loop launch: ") + hipGetErrorString(e));

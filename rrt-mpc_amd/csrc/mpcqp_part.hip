@@ -9,90 +9,105 @@
 namespace mpcqp {
 #if MPCQP_PART_LO <= 1 && 1 <= MPCQP_PART_HI
 template void launch_solve<1>(hipStream_t, const Launch&);
+template bool launch_solve_pair<1>(hipStream_t, const Launch&);
 template void launch_serve<1>(hipStream_t, const mpcqp_params&, const ServeLaunch&);
 template void launch_fleet_loop<1>(hipStream_t, const mpcqp_params*, const mpcqp_fleet&, int,
                                            const LoopTrigger&);
 #endif
 #if MPCQP_PART_LO <= 2 && 2 <= MPCQP_PART_HI
 template void launch_solve<2>(hipStream_t, const Launch&);
+template bool launch_solve_pair<2>(hipStream_t, const Launch&);
 template void launch_serve<2>(hipStream_t, const mpcqp_params&, const ServeLaunch&);
 template void launch_fleet_loop<2>(hipStream_t, const mpcqp_params*, const mpcqp_fleet&, int,
                                            const LoopTrigger&);
 #endif
 #if MPCQP_PART_LO <= 3 && 3 <= MPCQP_PART_HI
 template void launch_solve<3>(hipStream_t, const Launch&);
+template bool launch_solve_pair<3>(hipStream_t, const Launch&);
 template void launch_serve<3>(hipStream_t, const mpcqp_params&, const ServeLaunch&);
 template void launch_fleet_loop<3>(hipStream_t, const mpcqp_params*, const mpcqp_fleet&, int,
                                            const LoopTrigger&);
 #endif
 #if MPCQP_PART_LO <= 4 && 4 <= MPCQP_PART_HI
 template void launch_solve<4>(hipStream_t, const Launch&);
+template bool launch_solve_pair<4>(hipStream_t, const Launch&);
 template void launch_serve<4>(hipStream_t, const mpcqp_params&, const ServeLaunch&);
 template void launch_fleet_loop<4>(hipStream_t, const mpcqp_params*, const mpcqp_fleet&, int,
                                            const LoopTrigger&);
 #endif
 #if MPCQP_PART_LO <= 5 && 5 <= MPCQP_PART_HI
 template void launch_solve<5>(hipStream_t, const Launch&);
+template bool launch_solve_pair<5>(hipStream_t, const Launch&);
 template void launch_serve<5>(hipStream_t, const mpcqp_params&, const ServeLaunch&);
 template void launch_fleet_loop<5>(hipStream_t, const mpcqp_params*, const mpcqp_fleet&, int,
                                            const LoopTrigger&);
 #endif
 #if MPCQP_PART_LO <= 6 && 6 <= MPCQP_PART_HI
 template void launch_solve<6>(hipStream_t, const Launch&);
+template bool launch_solve_pair<6>(hipStream_t, const Launch&);
 template void launch_serve<6>(hipStream_t, const mpcqp_params&, const ServeLaunch&);
 template void launch_fleet_loop<6>(hipStream_t, const mpcqp_params*, const mpcqp_fleet&, int,
                                            const LoopTrigger&);
 #endif
 #if MPCQP_PART_LO <= 7 && 7 <= MPCQP_PART_HI
 template void launch_solve<7>(hipStream_t, const Launch&);
+template bool launch_solve_pair<7>(hipStream_t, const Launch&);
 template void launch_serve<7>(hipStream_t, const mpcqp_params&, const ServeLaunch&);
 template void launch_fleet_loop<7>(hipStream_t, const mpcqp_params*, const mpcqp_fleet&, int,
                                            const LoopTrigger&);
 #endif
 #if MPCQP_PART_LO <= 8 && 8 <= MPCQP_PART_HI
 template void launch_solve<8>(hipStream_t, const Launch&);
+template bool launch_solve_pair<8>(hipStream_t, const Launch&);
 template void launch_serve<8>(hipStream_t, const mpcqp_params&, const ServeLaunch&);
 template void launch_fleet_loop<8>(hipStream_t, const mpcqp_params*, const mpcqp_fleet&, int,
                                            const LoopTrigger&);
 #endif
 #if MPCQP_PART_LO <= 9 && 9 <= MPCQP_PART_HI
 template void launch_solve<9>(hipStream_t, const Launch&);
+template bool launch_solve_pair<9>(hipStream_t, const Launch&);
 template void launch_serve<9>(hipStream_t, const mpcqp_params&, const ServeLaunch&);
 template void launch_fleet_loop<9>(hipStream_t, const mpcqp_params*, const mpcqp_fleet&, int,
                                            const LoopTrigger&);
 #endif
 #if MPCQP_PART_LO <= 10 && 10 <= MPCQP_PART_HI
 template void launch_solve<10>(hipStream_t, const Launch&);
+template bool launch_solve_pair<10>(hipStream_t, const Launch&);
 template void launch_serve<10>(hipStream_t, const mpcqp_params&, const ServeLaunch&);
 template void launch_fleet_loop<10>(hipStream_t, const mpcqp_params*, const mpcqp_fleet&, int,
                                            const LoopTrigger&);
 #endif
 #if MPCQP_PART_LO <= 11 && 11 <= MPCQP_PART_HI
 template void launch_solve<11>(hipStream_t, const Launch&);
+template bool launch_solve_pair<11>(hipStream_t, const Launch&);
 template void launch_serve<11>(hipStream_t, const mpcqp_params&, const ServeLaunch&);
 template void launch_fleet_loop<11>(hipStream_t, const mpcqp_params*, const mpcqp_fleet&, int,
                                            const LoopTrigger&);
 #endif
 #if MPCQP_PART_LO <= 12 && 12 <= MPCQP_PART_HI
 template void launch_solve<12>(hipStream_t, const Launch&);
+template bool launch_solve_pair<12>(hipStream_t, const Launch&);
 template void launch_serve<12>(hipStream_t, const mpcqp_params&, const ServeLaunch&);
 template void launch_fleet_loop<12>(hipStream_t, const mpcqp_params*, const mpcqp_fleet&, int,
                                            const LoopTrigger&);
 #endif
 #if MPCQP_PART_LO <= 13 && 13 <= MPCQP_PART_HI
 template void launch_solve<13>(hipStream_t, const Launch&);
+template bool launch_solve_pair<13>(hipStream_t, const Launch&);
 template void launch_serve<13>(hipStream_t, const mpcqp_params&, const ServeLaunch&);
 template void launch_fleet_loop<13>(hipStream_t, const mpcqp_params*, const mpcqp_fleet&, int,
                                            const LoopTrigger&);
 #endif
 #if MPCQP_PART_LO <= 14 && 14 <= MPCQP_PART_HI
 template void launch_solve<14>(hipStream_t, const Launch&);
+template bool launch_solve_pair<14>(hipStream_t, const Launch&);
 template void launch_serve<14>(hipStream_t, const mpcqp_params&, const ServeLaunch&);
 template void launch_fleet_loop<14>(hipStream_t, const mpcqp_params*, const mpcqp_fleet&, int,
                                            const LoopTrigger&);
 #endif
 #if MPCQP_PART_LO <= 15 && 15 <= MPCQP_PART_HI
 template void launch_solve<15>(hipStream_t, const Launch&);
+template bool launch_solve_pair<15>(hipStream_t, const Launch&);
 template void launch_serve<15>(hipStream_t, const mpcqp_params&, const ServeLaunch&);
 template void launch_fleet_loop<15>(hipStream_t, const mpcqp_params*, const mpcqp_fleet&, int,
                                            const LoopTrigger&);

@@ -69,8 +69,9 @@ struct SolveLds {
 //   slot 2  c20 x_p + c21 x_{p-2} + c22 x_{p-4}         (a_j - a_{j-1}; delta_j - delta_{j-1})
 // with c = (row scaling E x row coefficient) x the column scaling D of the variable it multiplies:
 // the scaled operator Cbar = E C D with D folded into the coefficients.
-template <int N>
+template <int N, bool Pair = false>
 struct Ctx {
+  using LN = Lanes<Pair>;
   static constexpr int n = 2 * N;
   int lane;
   bool act, even;
@@ -118,12 +119,12 @@ struct Ctx {
   // instructions, ~110 cycles).  Staging through LDS instead (one ds_write + kNW ds_reads, no VALU
   // work) measured slower (+3 % at B = 4096, +9 % at B = 512): its round trip is on every product's
   // critical path.
-  __device__ __forceinline__ void vbcast(double v, double w[4]) const { bcast<kNW>(v, w); }
+  __device__ __forceinline__ void vbcast(double v, double w[4]) const { LN::template vbcast<kNW>(v, w); }
 
   // z = Cbar x: shifts only (no scans)
   __device__ __forceinline__ void Cmul(double x, double z[3]) const {
-    const double xm2 = shr2(x);
-    const double xm4 = shr2(xm2);
+    const double xm2 = LN::shr2(x);
+    const double xm4 = LN::shr2(xm2);
     z[0] = c0 * x;
     z[1] = c10 * x + c11 * xm2;
     z[2] = (c20 * x + c21 * xm2) + c22 * xm4;
@@ -133,7 +134,7 @@ struct Ctx {
     const double a = c11 * y[1] + c21 * y[2];  // to the variable 2 back
     const double b = c22 * y[2];               // to the variable 4 back
     const double t = (c0 * y[0] + c10 * y[1]) + c20 * y[2];
-    return t + shl2(a + shl2(b));
+    return t + LN::shl2(a + LN::shl2(b));
   }
   // (Pbar v)_lane, Pbar symmetric: lane reads its row as a conflict-free column of the LDS copy
   // The column loads go out in groups of kPG ahead of their FMAs (the inline-asm FMAs pin each
@@ -200,10 +201,10 @@ struct Ctx {
     // own rows' c_0 terms, lane p+2's c_1 terms and lane p+4's c_2 terms, and so on
     const double a1 = rw[1] * c11, a2 = rw[2] * c21, b2 = rw[2] * c22;
     const double dg = (c0 * c0 * rw[0] + rw[1] * c10 * c10) + rw[2] * c20 * c20;
-    const double b0 = (dg + shl2(a1 * c11 + a2 * c21) + shl4(b2 * c22)) + s;
-    const double bp2 = shl2(a1 * c10 + a2 * c20) + shl4(b2 * c21);  // entry (p, p+2)
-    const double bp4 = shl4(b2 * c20);                               // entry (p, p+4)
-    const double bm2 = shr2(bp2), bm4 = shr4(bp4);  // symmetric: (p, p-2) = lane p-2's (., +2)
+    const double b0 = (dg + LN::shl2(a1 * c11 + a2 * c21) + LN::shl4(b2 * c22)) + s;
+    const double bp2 = LN::shl2(a1 * c10 + a2 * c20) + LN::shl4(b2 * c21);  // entry (p, p+2)
+    const double bp4 = LN::shl4(b2 * c20);                                   // entry (p, p+4)
+    const double bm2 = LN::shr2(bp2), bm4 = LN::shr4(bp4);  // symmetric: (p, p-2) = lane p-2's (., +2)
     const bool live = ln < n;
     if constexpr (kPackedP<N>) {
       // lower band entries only: lane p adds into (p, p - 4), (p, p - 2), (p, p); the upper ones
@@ -298,9 +299,14 @@ struct Ctx {
       // the pivot A[k][k] (lane k's r[k]): by readlane, so 1/d is computed while the column's
       // broadcast is in flight; then a vector reciprocal (v_rcp_f64 + two Newton steps, within an
       // ulp of 1/d): no IEEE division sequence on the step's critical path
-      const double d = readlane(r[k], k);
-      double w[4];
-      vbcast(r[k], w);
+      double d, w[4];
+      if constexpr (Pair) {  // the half's lane k, from its broadcast row
+        vbcast(r[k], w);
+        d = row_bc<k % 16>(w[k / 16]);
+      } else {
+        d = readlane(r[k], k);
+        vbcast(r[k], w);
+      }
       ok = ok && (d > 0.0) && isfinite(d);
       double inv = __builtin_amdgcn_rcp(d);
       inv = fma(inv, fma(-d, inv, 1.0), inv);
@@ -323,18 +329,19 @@ struct Ctx {
   // kappa = delta / (1 + delta c'u).  Used by the polish when a few soft rows enter or leave
   // the active set.  false (inverse untouched) when 1 + delta c'u is not safely positive.
   __device__ __forceinline__ bool rank1(int tau, int l, double delta) {
-    const int lu = __builtin_amdgcn_readfirstlane(l);
+    const int lu = LN::uniform(l);
     // the row's coefficients on the variables lu, lu-2, lu-4 (lane lu's c)
-    const double k0 = readlane(tau == 0 ? c0 : (tau == 1 ? c10 : c20), lu);
-    const double k1 = lu >= 2 ? readlane(tau == 1 ? c11 : (tau == 2 ? c21 : 0.0), lu) : 0.0;
-    const double k2 = lu >= 4 ? readlane(tau == 2 ? c22 : 0.0, lu) : 0.0;
+    const double k0 = LN::readv(tau == 0 ? c0 : (tau == 1 ? c10 : c20), lu);
+    const double k1 = lu >= 2 ? LN::readv(tau == 1 ? c11 : (tau == 2 ? c21 : 0.0), lu) : 0.0;
+    const double k2 = lu >= 4 ? LN::readv(tau == 2 ? c22 : 0.0, lu) : 0.0;
     // u = A^{-1} c: c has at most three entries, so u is three columns of the inverse -- by
     // symmetry the lane's own registers r[lu], r[lu-2], r[lu-4] (A^{-1}[i][j] = -r_i[j])
     double u = k0 * pick<0, n>(lu);
     if (lu >= 2) u += k1 * pick<0, n>(lu - 2);
     if (lu >= 4) u += k2 * pick<0, n>(lu - 4);
     u = act ? -u : 0.0;
-    const double cu = (k0 * readlane(u, lu) + k1 * readlane(u, lu >= 2 ? lu - 2 : 0)) + k2 * readlane(u, lu >= 4 ? lu - 4 : 0);
+    const double cu = (k0 * LN::readv(u, lu) + k1 * LN::readv(u, lu >= 2 ? lu - 2 : 0)) +
+                      k2 * LN::readv(u, lu >= 4 ? lu - 4 : 0);
     const double den = 1.0 + delta * cu;
     if (!(den > kRank1Min) || !isfinite(den)) return false;
     const double m = (delta / den) * u;
@@ -434,11 +441,12 @@ struct ServeWin {
 //   slot 1: input row        a_{p/2} or delta_{p/2}                    (:83-86)
 //   slot 2: rate row         U_p - U_{p-2} (u_prev at k = 0)           (:89-106)
 // the constant parts (v_0 = x0[3], u_prev) moved into the bounds.
-template <int N, class Win>
+template <int N, class Win, bool Pair = false>
 __device__ __forceinline__ bool setup_qp(const mpcqp_params& p, int b, const double* __restrict__ model,
                                          const double* __restrict__ in_x0, const double* __restrict__ in_ref,
-                                         const double* __restrict__ in_up, const Win& win, Ctx<N>& C, SolveLds<N>& lds,
-                                         double* __restrict__ scratch, double* __restrict__ dbg) {
+                                         const double* __restrict__ in_up, const Win& win, Ctx<N, Pair>& C,
+                                         SolveLds<N>& lds, double* __restrict__ scratch, double* __restrict__ dbg) {
+  using LN = Lanes<Pair>;
   constexpr int n = 2 * N;
   SetupSmem<N>& sm = lds.setup;
   (void)scratch;
@@ -455,7 +463,7 @@ __device__ __forceinline__ bool setup_qp(const mpcqp_params& p, int b, const dou
   if constexpr (Win::kFleet) {  // the fleet loop: the vehicle's window -> LTV model into LDS
     double rx = 0.0, ry = 0.0, ryaw = 0.0, rv = 0.0;
     if (lane <= N) win.template row<N>(lane, rx, ry, ryaw, rv);
-    build_qp(p, lane, rx, ry, ryaw, rv, win.x0l(lane), win.upl(lane), lds.model_ptr());
+    build_qp<Pair>(p, lane, rx, ry, ryaw, rv, win.x0l(lane), win.upl(lane), lds.model_ptr());
   } else if (in_ref) {  // K1 fused: the window -> LTV model straight into LDS (mpcqp_build.h)
     const double* rb = in_ref + (size_t)b * (N + 1) * 4;
     double rx = 0.0, ry = 0.0, ryaw = 0.0, rv = 0.0;
@@ -467,11 +475,11 @@ __device__ __forceinline__ bool setup_qp(const mpcqp_params& p, int b, const dou
     }
     const double x0l = lane < 4 ? in_x0[(size_t)b * 4 + lane] : 0.0;
     const double upl = (lane >= 4 && lane < 6 && in_up) ? in_up[(size_t)b * 2 + lane - 4] : 0.0;
-    build_qp(p, lane, rx, ry, ryaw, rv, x0l, upl, lds.model_ptr());
+    build_qp<Pair>(p, lane, rx, ry, ryaw, rv, x0l, upl, lds.model_ptr());
   } else {
     const double* mb = model + (size_t)b * S;
     double* md = lds.model_ptr();
-    for (int i = lane; i < S; i += kWave) md[i] = mb[i];
+    for (int i = lane; i < S; i += LN::kLanes) md[i] = mb[i];
   }
   __syncthreads();
   const double* mdl = lds.model_ptr();
@@ -780,12 +788,12 @@ __device__ __forceinline__ bool setup_qp(const mpcqp_params& p, int b, const dou
     // column norms of [P; A] (first n columns of the KKT matrix): the lane's own rows and
     // the banded rows 2 and 4 ahead
     double ccol = fmax(fmax(E[0], E[1] * fabs(k1[0])), E[2] * fabs(k2[0]));
-    ccol = fmax(ccol, shl2(fmax(E[1] * fabs(k1[1]), E[2] * fabs(k2[1]))));
-    ccol = fmax(ccol, shl4(E[2] * fabs(k2[2])));
+    ccol = fmax(ccol, LN::shl2(fmax(E[1] * fabs(k1[1]), E[2] * fabs(k2[1]))));
+    ccol = fmax(ccol, LN::shl4(E[2] * fabs(k2[2])));
     ccol *= D;
     const double dl = act ? rsqrt(limit_scaling(fmax(cmax, ccol))) : 0.0;
     // row norms of A
-    const double Dm2 = shr2(D), Dm4 = shr2(Dm2);
+    const double Dm2 = LN::shr2(D), Dm4 = LN::shr2(Dm2);
     const double r1 = fmax(fabs(k1[0]) * D, fabs(k1[1]) * Dm2);
     const double r2 = fmax(fmax(fabs(k2[0]) * D, fabs(k2[1]) * Dm2), fabs(k2[2]) * Dm4);
     const double el0 = even ? rsqrt(limit_scaling(E[0] * D)) : 0.0;
@@ -810,8 +818,8 @@ __device__ __forceinline__ bool setup_qp(const mpcqp_params& p, int b, const dou
     E[1] *= el1;
     E[2] *= el2;
     // cost scaling
-    const double cn = wave_sum(act ? cm2 : 0.0) / n;
-    const double qn = limit_scaling(wave_max(fabs(qv)));
+    const double cn = LN::sum(act ? cm2 : 0.0) / n;
+    const double qn = limit_scaling(LN::max(fabs(qv)));
     const double ct = 1.0 / limit_scaling(fmax(cn, qn));
     cpend = ct;
     qv *= ct;
@@ -882,13 +890,13 @@ __device__ __forceinline__ bool setup_qp(const mpcqp_params& p, int b, const dou
     finite = finite && isfinite(lo[r]) && isfinite(hi[r]);
   }
   // non-finite data (NaN/inf in x0, ref or u_prev) -> status MPCQP_NUMERICAL_ERROR
-  const bool bad_input = wave_any(!finite);
+  const bool bad_input = LN::any(!finite);
   C.init(lane, dt, lds.solve);
   C.qv = qv;
   C.D = D;
   C.cscale = cscale;
   {  // Cbar's coefficients: row scaling x row coefficient x the column scaling of the variable
-    const double Dm2 = shr2(D), Dm4 = shr2(Dm2);
+    const double Dm2 = LN::shr2(D), Dm4 = LN::shr2(Dm2);
     C.c0 = E[0] * D;
     C.c10 = (E[1] * k1[0]) * D;
     C.c11 = (E[1] * k1[1]) * Dm2;
@@ -942,9 +950,10 @@ __device__ __forceinline__ bool setup_qp(const mpcqp_params& p, int b, const dou
 // reproduces itself (the exact optimum: returns 1, x = that optimum); otherwise an exact line
 // search along the Newton step.  0: not found within max_it passes, -1: numerical failure.
 // Uses the KKT inverse registers (an ADMM phase that continues must refactor).
-template <int N>
-__device__ __forceinline__ int polish_qp(Ctx<N>& C, double& x, const double zg[3], int max_it, int& pol_it,
+template <int N, bool Pair = false>
+__device__ __forceinline__ int polish_qp(Ctx<N, Pair>& C, double& x, const double zg[3], int max_it, int& pol_it,
                                          int& nfact, int& n_ls) {
+  using LN = Lanes<Pair>;
   constexpr int n = 2 * N;
   const bool act = C.act;
   int result = 0;
@@ -975,7 +984,7 @@ __device__ __forceinline__ int polish_qp(Ctx<N>& C, double& x, const double zg[3
       int nchg = 0;
 #pragma unroll
       for (int r = 0; r < 3; ++r) {
-        chg[r] = __ballot(act && rw[r] != rwf[r]);
+        chg[r] = LN::ballot(act && rw[r] != rwf[r]);
         nchg += __popcll(chg[r]);
       }
       refac = nchg > kMaxRank1;
@@ -986,7 +995,7 @@ __device__ __forceinline__ int polish_qp(Ctx<N>& C, double& x, const double zg[3
         while (m && !refac) {
           const int l = __builtin_ctzll(m);
           m &= m - 1;
-          refac = !C.rank1(r, l, readlane(rw[r] - rwf[r], l));
+          refac = !C.rank1(r, l, LN::readv(rw[r] - rwf[r], l));
           ++C.n_r1;
         }
       }
@@ -1000,7 +1009,7 @@ __device__ __forceinline__ int polish_qp(Ctx<N>& C, double& x, const double zg[3
       const bool okf = C.sweep();
       T.end(1);
       ++C.n_full;
-      if (wave_any(!okf)) {
+      if (LN::any(!okf)) {
         result = -1;
         break;
       }
@@ -1020,12 +1029,12 @@ __device__ __forceinline__ int polish_qp(Ctx<N>& C, double& x, const double zg[3
       const int c2 = zn[r] > C.hi[r] ? 2 : (zn[r] < C.lo[r] ? 1 : 0);
       diff = diff || (c2 != cd[r]);
     }
-    if (wave_any(!isfinite(xn))) {
+    if (LN::any(!isfinite(xn))) {
       T.end(2);
       result = -1;
       break;
     }
-    if (!wave_any(diff)) {
+    if (!LN::any(diff)) {
       // the set reproduces itself: one step of iterative refinement (res = rhs - M xn), then
       // accept if it still does
       double t3[3];
@@ -1040,12 +1049,12 @@ __device__ __forceinline__ int polish_qp(Ctx<N>& C, double& x, const double zg[3
         const int c2 = zn[r] > C.hi[r] ? 2 : (zn[r] < C.lo[r] ? 1 : 0);
         diff = diff || (c2 != cd[r]);
       }
-      if (wave_any(!isfinite(xn))) {
+      if (LN::any(!isfinite(xn))) {
         T.end(2);
         result = -1;
         break;
       }
-      if (!wave_any(diff)) {
+      if (!LN::any(diff)) {
         T.end(2);
         x = xn;
         result = 1;
@@ -1067,8 +1076,8 @@ __device__ __forceinline__ int polish_qp(Ctx<N>& C, double& x, const double zg[3
     double zd[3];
 #pragma unroll
     for (int r = 0; r < 3; ++r) zd[r] = zn[r] - zc[r];
-    const double qd = wave_sum(act ? dx * Pd : 0.0);
-    const double lin = wave_sum(act ? (Px + C.qv) * dx : 0.0);
+    const double qd = LN::sum(act ? dx * Pd : 0.0);
+    const double lin = LN::sum(act ? (Px + C.qv) * dx : 0.0);
     double t = 1.0;
     for (int ls = 0; ls < 40; ++ls) {
       ++n_ls;
@@ -1080,8 +1089,8 @@ __device__ __forceinline__ int polish_qp(Ctx<N>& C, double& x, const double zg[3
         g1 += 2.0 * C.wb[r] * rr * zd[r];
         if (rr != 0.0) g2 += 2.0 * C.wb[r] * zd[r] * zd[r];
       }
-      const double d1 = lin + t * qd + wave_sum(g1);
-      const double d2 = qd + wave_sum(g2);
+      const double d1 = lin + t * qd + LN::sum(g1);
+      const double d2 = qd + LN::sum(g2);
       if (d1 <= 0.0 || !(d2 > 0.0)) break;
       const double tn = fmax(0.0, t - d1 / d2);
       if (tn >= t) break;
@@ -1095,7 +1104,7 @@ __device__ __forceinline__ int polish_qp(Ctx<N>& C, double& x, const double zg[3
         moved = moved || ca != cb;
       }
       t = tn;
-      if (!wave_any(moved)) break;
+      if (!LN::any(moved)) break;
     }
     x = x + t * dx;
     Px = Px + t * Pd;
@@ -1129,8 +1138,9 @@ enum : int { kAdmmBad = -1, kAdmmMaxIter = 0, kAdmmConverged = 1, kAdmmApprox = 
 // kAdmmAttempt (a check asks for an early polish; rho_change/rho_next hold that check's
 // adaptive-rho decision), kAdmmApprox / kAdmmMaxIter (max_iter reached within / outside 10x the
 // tolerances: OSQP's solved_inaccurate / max_iter_reached).
-template <int N>
-__device__ __forceinline__ int admm_run(const mpcqp_params& p, Ctx<N>& C, AdmmState& S) {
+template <int N, bool Pair = false>
+__device__ __forceinline__ int admm_run(const mpcqp_params& p, Ctx<N, Pair>& C, AdmmState& S) {
+  using LN = Lanes<Pair>;
   const bool act = C.act;
   const double sg = p.sigma, alpha = p.alpha;
   const bool early = p.polish != 0 && p.polish_from > 0;
@@ -1147,7 +1157,7 @@ __device__ __forceinline__ int admm_run(const mpcqp_params& p, Ctx<N>& C, AdmmSt
       T.begin();
       const bool okf = C.sweep();
       T.end(1);
-      if (wave_any(!okf)) {
+      if (LN::any(!okf)) {
         ev = kAdmmBad;
         break;
       }
@@ -1207,10 +1217,10 @@ __device__ __forceinline__ int admm_run(const mpcqp_params& p, Ctx<N>& C, AdmmSt
             snprim = fmax(snprim, fmax(fabs(Ax[r]), fabs(S.z[r])));
           }
         }
-        pr = wave_max(pr);
-        nprim = wave_max(nprim);
-        spr = wave_max(spr);
-        snprim = wave_max(snprim);
+        pr = LN::max(pr);
+        nprim = LN::max(nprim);
+        spr = LN::max(spr);
+        snprim = LN::max(snprim);
         const double Px = C.Pmul(x);
         const double Aty = C.CTmul(S.y);
         double du = 0, ndual = 0, sdu = 0, sndual = 0;
@@ -1222,17 +1232,17 @@ __device__ __forceinline__ int admm_run(const mpcqp_params& p, Ctx<N>& C, AdmmSt
           sdu = fabs(rd);
           sndual = fmax(fmax(fabs(Px), fabs(Aty)), fabs(C.qv));
         }
-        du = wave_max(du);
-        ndual = wave_max(ndual);
-        sdu = wave_max(sdu);
-        sndual = wave_max(sndual);
+        du = LN::max(du);
+        ndual = LN::max(ndual);
+        sdu = LN::max(sdu);
+        sndual = LN::max(sndual);
         const double ic = 1.0 / C.cscale;
         du *= ic;
         const double ep = p.eps_abs + p.eps_rel * nprim;
         const double ed = p.eps_abs + p.eps_rel * ndual * ic;
         T.end(3);
         // fmax drops NaNs, so test the iterate itself
-        if (wave_any(!isfinite(x) || !isfinite(S.z[0] + S.z[1] + S.z[2]) || !isfinite(S.y[0] + S.y[1] + S.y[2])) ||
+        if (LN::any(!isfinite(x) || !isfinite(S.z[0] + S.z[1] + S.z[2]) || !isfinite(S.y[0] + S.y[1] + S.y[2])) ||
             !isfinite(pr) || !isfinite(du)) {
           ev = kAdmmBad;
           done = true;
@@ -1297,16 +1307,17 @@ __device__ __forceinline__ void admm_debug_state(double* __restrict__ dbg, bool 
 // ------------------------------------------------------------------ K2c: status + outputs
 // x: the returned iterate (the polish's last iterate when the final polish ran), x_admm: the
 // ADMM iterate (returned when that polish did not converge, as OSQP does).
-template <int N, class Win>
+template <int N, class Win, bool Pair = false>
 __device__ __forceinline__ int finish_qp(const mpcqp_params& p, int b, const double* __restrict__ model,
                                          const double* __restrict__ in_x0, const double* __restrict__ in_ref,
                                          const double* __restrict__ in_up, const Win& win, const double* kept_model,
-                                         Ctx<N>& C,
+                                         Ctx<N, Pair>& C,
                                           double x, double x_admm, int admm_flag, bool do_polish, bool pol_ok,
                                           bool bad, int admm_it, int nfact, int pol_it, int n_ls,
                                           double* __restrict__ u0o, double* __restrict__ Xo, double* __restrict__ Uo,
                                           int32_t* __restrict__ statuso, int32_t* __restrict__ iterso,
                                           uint8_t* __restrict__ activeo, double& Uout) {
+  using LN = Lanes<Pair>;
   constexpr int n = 2 * N;
   const int lane = win.lane();
   const bool act = C.act;
@@ -1315,7 +1326,7 @@ __device__ __forceinline__ int finish_qp(const mpcqp_params& p, int b, const dou
   const bool admm_ok = admm_flag == kAdmmConverged;
   Stamps T3;
   T3.begin();
-  if (wave_any(!isfinite(x))) bad = true;
+  if (LN::any(!isfinite(x))) bad = true;
   int status;
   if (bad) {
     status = MPCQP_NUMERICAL_ERROR;
@@ -1353,7 +1364,7 @@ __device__ __forceinline__ int finish_qp(const mpcqp_params& p, int b, const dou
   } else if constexpr (Win::kFleet) {
     double rx = 0.0, ry = 0.0, ryaw = 0.0, rv = 0.0;
     if (lane <= N) win.template row<N>(lane, rx, ry, ryaw, rv);
-    const LaneModel m = build_lane(p, lane, ryaw, rv);
+    const LaneModel m = build_lane<Pair>(p, lane, ryaw, rv);
     m_al = m.al;
     m_be = m.be;
     m_ga = m.ga;
@@ -1370,7 +1381,7 @@ __device__ __forceinline__ int finish_qp(const mpcqp_params& p, int b, const dou
   } else if (in_ref) {
     const double* rb = in_ref + (size_t)b * (N + 1) * 4;
     const double ryaw = lane <= N ? rb[4 * lane + 2] : 0.0, rv = lane <= N ? rb[4 * lane + 3] : 0.0;
-    const LaneModel m = build_lane(p, lane, ryaw, rv);
+    const LaneModel m = build_lane<Pair>(p, lane, ryaw, rv);
     m_al = m.al;
     m_be = m.be;
     m_ga = m.ga;
@@ -1405,16 +1416,16 @@ __device__ __forceinline__ int finish_qp(const mpcqp_params& p, int b, const dou
   const int cc = lane & 1;
   const double W = act ? C.D * x : 0.0;  // v_{j+1} on lane 2j, delta_j on lane 2j+1
   const double dt = p.dt;
-  const double Wm2 = shr2(W);
+  const double Wm2 = LN::shr2(W);
   const double U = !act ? 0.0 : (cc == 1 ? W : (W - (lane == 0 ? x03 : Wm2)) / dt);
-  const double sj_all = __shfl(m_si, lane >> 1, kWave);
+  const double sj_all = LN::shfl(m_si, lane >> 1);
   const double sj = act ? sj_all : 0.0;
   // psi_{j+1} on lane 2j+1
-  const double sacc = scan_add((act && cc == 1) ? sj * U : 0.0, lane);
+  const double sacc = LN::scan((act && cc == 1) ? sj * U : 0.0, lane);
   // lane k <- (psi_k, v_k)
   const int srcv = lane == 0 ? 0 : 2 * (lane - 1);
-  const double vk_s = __shfl(W, srcv < kWave ? srcv : 0, kWave);
-  const double pk_s = __shfl(sacc, (srcv + 1) < kWave ? srcv + 1 : 0, kWave);
+  const double vk_s = LN::shfl(W, srcv < LN::kLanes ? srcv : 0);
+  const double pk_s = LN::shfl(sacc, (srcv + 1) < LN::kLanes ? srcv + 1 : 0);
   const double vk = lane == 0 ? x03 : vk_s;
   const double pk = lane == 0 ? x02 : x02 + pk_s;
   double t0 = 0.0, t1 = 0.0;
@@ -1422,8 +1433,8 @@ __device__ __forceinline__ int finish_qp(const mpcqp_params& p, int b, const dou
     t0 = m_al * pk + m_be * vk + m_c0;
     t1 = m_ga * pk + m_et * vk + m_c1;
   }
-  const double in0 = scan_add(t0, lane), in1 = scan_add(t1, lane);
-  const double ex0 = dpp<kWaveShr1>(in0), ex1 = dpp<kWaveShr1>(in1);  // exclusive prefix
+  const double in0 = LN::scan(t0, lane), in1 = LN::scan(t1, lane);
+  const double ex0 = LN::shr1(in0), ex1 = LN::shr1(in1);  // exclusive prefix
   const double Xk0 = x00 + ex0, Xk1 = x01 + ex1;
   if (Xo && lane <= N) {
     double* Xb = Xo + (size_t)b * 4 * (N + 1);
@@ -1435,7 +1446,7 @@ __device__ __forceinline__ int finish_qp(const mpcqp_params& p, int b, const dou
   Uout = U;
   if (Uo && act) Uo[(size_t)b * n + cc * N + (lane >> 1)] = U;
   if (u0o && lane < 2) u0o[(size_t)b * 2 + lane] = U;
-  const double Um2 = shr2(U);
+  const double Um2 = LN::shr2(U);
   if (activeo) {
     uint8_t* ab = activeo + (size_t)b * (5 * N + 1);
     if (lane <= N) ab[lane] = vk > p.v_bounds[1] ? 2 : (vk < p.v_bounds[0] ? 1 : 0);
@@ -1462,7 +1473,7 @@ __device__ __forceinline__ int finish_qp(const mpcqp_params& p, int b, const dou
 // One QP through setup -> ADMM (+ early polish attempts) -> final polish -> outputs on the calling
 // wave, for the fused fleet loop (k_fleet_loop; no debug state): returns the status, Ulane = the
 // lane's U entry (lane 0/1: u0).  k_solve runs the same driver inline (below).
-template <int N, class Win>
+template <int N, class Win, bool Pair = false>
 __device__ __forceinline__ int solve_one(const mpcqp_params& p, int b, const double* __restrict__ model,
                                          const double* __restrict__ in_x0, const double* __restrict__ in_ref,
                                          const double* __restrict__ in_up, const Win& win, SolveLds<N>& sm,
@@ -1473,8 +1484,8 @@ __device__ __forceinline__ int solve_one(const mpcqp_params& p, int b, const dou
   const uint64_t t_start = __builtin_amdgcn_s_memtime();
   Stamps TK;
   TK.begin();
-  Ctx<N> C;
-  bool bad = setup_qp<N>(p, b, model, in_x0, in_ref, in_up, win, C, sm, nullptr, dbg);
+  Ctx<N, Pair> C;
+  bool bad = setup_qp<N, Win, Pair>(p, b, model, in_x0, in_ref, in_up, win, C, sm, nullptr, dbg);
   const bool use_admm = p.method == MPCQP_METHOD_ADMM;
   AdmmState S;
   S.x = 0.0;
@@ -1496,7 +1507,7 @@ __device__ __forceinline__ int solve_one(const mpcqp_params& p, int b, const dou
     int kind = 0;
     double zg[3];
     if (use_admm) {
-      const int ev = admm_run<N>(p, C, S);
+      const int ev = admm_run<N, Pair>(p, C, S);
       if (ev == kAdmmAttempt) {
         kind = 1;
       } else {
@@ -1518,7 +1529,7 @@ __device__ __forceinline__ int solve_one(const mpcqp_params& p, int b, const dou
     double xp = kind == 1 ? S.x : x;
     Stamps T2;
     T2.begin();
-    const int r_ = polish_qp<N>(C, xp, zg, kind == 1 ? p.polish_attempt_max_iter : p.polish_max_iter, pol_it,
+    const int r_ = polish_qp<N, Pair>(C, xp, zg, kind == 1 ? p.polish_attempt_max_iter : p.polish_max_iter, pol_it,
                                 S.nfact, n_ls);
     T2.end(0);
     T2.flush(12);  // g_stamps[12]: polish
@@ -1542,7 +1553,7 @@ __device__ __forceinline__ int solve_one(const mpcqp_params& p, int b, const dou
     if (S.rho_change) S.rho = S.rho_next;
     S.rho_change = false;
   }
-  const int status = finish_qp<N>(p, b, model, in_x0, in_ref, in_up, win, sm.model, C, x, x_admm, flag, do_polish, pol_ok, bad, S.it,
+  const int status = finish_qp<N, Win, Pair>(p, b, model, in_x0, in_ref, in_up, win, sm.model, C, x, x_admm, flag, do_polish, pol_ok, bad, S.it,
                                   S.nfact, pol_it, n_ls, u0o, Xo, Uo, statuso, iterso, activeo, Ulane);
   TK.end(0);
   TK.flush(22);  // g_stamps[22]: the whole QP
@@ -1671,6 +1682,34 @@ __global__ __launch_bounds__(kWave, kSolveWavesPerEU<N>) void k_solve(mpcqp_para
   }
 }
 
+// ------------------------------------------------------------------ K2, two QPs per wave
+// N <= 15 (n <= 30 live lanes): lanes 0-31 solve QP 2w, lanes 32-63 QP 2w + 1 of workgroup w, each
+// half through solve_one's driver with the half-wave lane policy (Lanes<true>) and its own LDS
+// block; every operation of a QP is the one-wave kernel's, on the same values, so the results are
+// the same bit for bit.  The two QPs of a wave run in lockstep while both iterate and mask each other
+// off where they part (one polishes, one still iterates): the wave costs about the slower of its
+// QPs, and a batch needs half the waves.  Fused K1 only (no workspace model, no debug state).
+template <int N>
+__global__ __launch_bounds__(kWave, kSolveWavesPerEU<N>) void k_solve_pair(mpcqp_params p, int B,
+                                                      const uint8_t* __restrict__ mask,
+                                                      const double* __restrict__ in_x0,
+                                                      const double* __restrict__ in_ref,
+                                                      const double* __restrict__ in_up,
+                                                      double* __restrict__ u0o, double* __restrict__ Xo,
+                                                      double* __restrict__ Uo, int32_t* __restrict__ statuso,
+                                                      int32_t* __restrict__ iterso, uint8_t* __restrict__ activeo) {
+  static_assert(2 * N <= 30, "two QPs per wave need n = 2N <= 30 (a padding lane or two per half)");
+  __shared__ SolveLds<N> sm[2];
+  const int h = threadIdx.x >> 5;
+  const int b = 2 * blockIdx.x + h;
+  if (b >= B || (mask && !mask[b])) return;  // that half only: the other QP runs on
+  int ln = threadIdx.x & 31;
+  asm volatile("" : "+v"(ln));
+  double U;
+  solve_one<N, ServeWin, true>(p, b, nullptr, in_x0, in_ref, in_up, ServeWin{ln}, sm[h], u0o, Xo, Uo, statuso,
+                               iterso, activeo, U);
+}
+
 // ------------------------------------------------------------------ fused closed loop
 // Every vehicle of a fleet runs `steps` iterations of the loop body of TrajectoryTracker.track
 // (control_stage.py:100-150) on its own wave, with no kernel boundary between steps: the window
@@ -1679,14 +1718,22 @@ __global__ __launch_bounds__(kWave, kSolveWavesPerEU<N>) void k_solve(mpcqp_para
 // (:147-150) -- the operations of k_fleet_build / k_solve / k_fleet_advance (mpcqp_fleet.hip) in the
 // same order, so the traces equal mpcqp_fleet_run's bit for bit.  The loop state (x, u_prev) stays
 // in LDS across steps (no registers held through the solve); it is written back at the end.
-template <int N>
+// Pair: two vehicles per wave (N <= 15; lanes 0-31 / 32-63, as k_solve_pair), each half its own
+// loop state, LDS block and control flow.
+template <int N, bool Pair = false>
 __global__ __launch_bounds__(kWave, kSolveWavesPerEU<N>) void k_fleet_loop(const mpcqp_params* __restrict__ P,
                                                                          mpcqp_fleet f, int steps,
                                                                          mpcqp::LoopTrigger tr) {
-  __shared__ SolveLds<N> sm;
-  __shared__ double ls[6];  // loop state: x[4], u_prev[2]
-  const int b = tr.order ? tr.order[blockIdx.x] : (int)blockIdx.x;
-  const int lane = threadIdx.x;
+  using LN = Lanes<Pair>;
+  __shared__ SolveLds<N> smv[Pair ? 2 : 1];
+  __shared__ double lsv[Pair ? 12 : 6];  // loop state: x[4], u_prev[2] (per half)
+  const int h = Pair ? (int)(threadIdx.x >> 5) : 0;
+  SolveLds<N>& sm = smv[h];
+  double* const ls = lsv + 6 * h;
+  const int slot = 2 * (int)blockIdx.x + h;  // pair: may be V (odd V)
+  const int b = Pair ? ((tr.order && slot < f.vehicles) ? tr.order[slot] : slot)
+                     : (tr.order ? tr.order[blockIdx.x] : (int)blockIdx.x);
+  const int lane = Pair ? (int)(threadIdx.x & 31) : (int)threadIdx.x;
   const int V = f.vehicles;
   if (b >= V) return;
   int phase = f.phase[b];
@@ -1736,8 +1783,9 @@ __global__ __launch_bounds__(kWave, kSolveWavesPerEU<N>) void k_fleet_loop(const
       const mpcqp_params& p = P[relax];  // P = {nominal, relaxed} in global memory (ws->dparams)
       FleetWin win{rows, ln, len, pidx, relax != 0, {ls[0], ls[1], ls[2], ls[3]}, {ls[4], ls[5]}};
       double Ul;
-      const int st = solve_one<N>(p, b, nullptr, nullptr, nullptr, nullptr, win, sm, f.u0 + (size_t)relax * V * 2, f.X, nullptr,
-                                  f.status + (size_t)relax * V, nullptr, nullptr, Ul);
+      const int st = solve_one<N, FleetWin, Pair>(p, b, nullptr, nullptr, nullptr, nullptr, win, sm,
+                                                  f.u0 + (size_t)relax * V * 2, f.X, nullptr,
+                                                  f.status + (size_t)relax * V, nullptr, nullptr, Ul);
       __syncthreads();  // the next solve (or step) reuses the LDS
       if (lane == 0) f.mask[(size_t)relax * V + b] = 1;
       if (st == MPCQP_SOLVED || st == MPCQP_SOLVED_INACCURATE) {
@@ -1752,7 +1800,7 @@ __global__ __launch_bounds__(kWave, kSolveWavesPerEU<N>) void k_fleet_loop(const
       break;
     }
     // k_fleet_advance (every lane computes the same values)
-    const double a = readlane(U, 0), delta = readlane(U, 1);
+    const double a = LN::readv(U, 0), delta = LN::readv(U, 1);
     double x[4] = {ls[0], ls[1], ls[2], ls[3]}, xn[4];
     plant(x, a, delta, P[0].dt, P[0].wheelbase_px, xn);
     if (lane == 0) {
@@ -1854,7 +1902,26 @@ void launch_solve(hipStream_t s, const Launch& L) {
 }
 template <int N>
 void launch_fleet_loop(hipStream_t s, const mpcqp_params* P, const mpcqp_fleet& f, int steps, const LoopTrigger& tr) {
+  if constexpr (2 * N <= 30) {
+    if (tr.pair) {
+      hipLaunchKernelGGL((k_fleet_loop<N, true>), dim3((f.vehicles + 1) / 2), dim3(kWave), 0, s, P, f, steps, tr);
+      return;
+    }
+  }
   hipLaunchKernelGGL(k_fleet_loop<N>, dim3(f.vehicles), dim3(kWave), 0, s, P, f, steps, tr);
+}
+// two QPs per wave (N <= 15, fused K1, no debug state); false: not available for this launch
+template <int N>
+bool launch_solve_pair(hipStream_t s, const Launch& L) {
+  if constexpr (2 * N <= 30) {
+    hipLaunchKernelGGL(k_solve_pair<N>, dim3((L.B + 1) / 2), dim3(kWave), 0, s, *L.p, L.B, L.mask, L.x0, L.ref,
+                       L.u_prev, L.u0, L.X, L.U, L.st, L.it, L.ac);
+    return true;
+  } else {
+    (void)s;
+    (void)L;
+    return false;
+  }
 }
 
 }  // namespace mpcqp

@@ -34,7 +34,10 @@ STATUS_NAMES = {
 
 # OSQP settings used by the reference (src/control/mpc_controller.py:121-131) plus the
 # OSQP defaults it relies on implicitly.
-ABI_VERSION = 7  # MPCQP_ABI_VERSION (include/mpcqp.h)
+ABI_VERSION = 8  # MPCQP_ABI_VERSION (include/mpcqp.h)
+# two QPs per wave for N <= 15 (mpcqp_set_pairing)
+PAIR_OFF, PAIR_ON, PAIR_AUTO = 0, 1, 2
+PAIRING_MODES = {"off": PAIR_OFF, "on": PAIR_ON, "auto": PAIR_AUTO}
 E_DEVICE = -6  # MPCQP_E_DEVICE: a fault surfaced at a stream synchronisation
 
 DEFAULT_SOLVER_SETTINGS = dict(
@@ -270,6 +273,7 @@ _SYMBOLS = {
                      ctypes.POINTER(ctypes.c_int32)], ctypes.c_int),
     "mpcqp_solve_staged": ([ctypes.c_void_p], ctypes.c_int),
     "mpcqp_solve_served": ([ctypes.c_void_p], ctypes.c_int),
+    "mpcqp_set_pairing": ([ctypes.c_void_p, ctypes.c_int], ctypes.c_int),
 }
 
 

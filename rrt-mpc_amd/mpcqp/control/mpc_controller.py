@@ -94,9 +94,13 @@ class BatchedMPCController:
     ``solve_batch(x0[B,4], ref[B,N+1,4], u_prev[B,2])`` runs K1 + K2 asynchronously on
     the current torch stream (or ``stream``).  Inputs may be numpy arrays (copied to the
     device) or float64 device tensors (used in place).
+
+    ``pairing`` ("auto", "on", "off"): two QPs per wave for horizons N <= 15 (``mpcqp_set_pairing``;
+    the same results bit for bit).  "auto" pairs a launch with more QPs than the GPU has wave slots.
     """
 
-    def __init__(self, params, max_batch: int, *, device=None, method: str = "admm", **settings) -> None:
+    def __init__(self, params, max_batch: int, *, device=None, method: str = "admm", pairing: str = "auto",
+                 **settings) -> None:
         import torch
 
         if method not in ("admm", "newton"):
@@ -120,6 +124,7 @@ class BatchedMPCController:
             _lib.check(L.mpcqp_create(ctypes.byref(self._cparams), self.max_batch, self.device.index, ctypes.byref(ws)),
                        "mpcqp_create")
         self._ws = ws
+        self.set_pairing(pairing)
         N, B = self.horizon, self.max_batch
         kw = dict(device=self.device)
         self._u0 = torch.empty((B, 2), dtype=torch.float64, **kw)
@@ -135,6 +140,13 @@ class BatchedMPCController:
         self._cparams = _lib.to_c_params(params, self.method, **self.settings)
         _lib.check(self._L.mpcqp_set_params(self._ws, ctypes.byref(self._cparams)), "mpcqp_set_params")
         self.params = params
+
+    def set_pairing(self, mode: str) -> None:
+        """Two QPs per wave for N <= 15: "auto" (default), "on" or "off" (mpcqp_set_pairing)."""
+        if mode not in _lib.PAIRING_MODES:
+            raise ValueError(f"pairing must be one of {sorted(_lib.PAIRING_MODES)}")
+        _lib.check(self._L.mpcqp_set_pairing(self._ws, _lib.PAIRING_MODES[mode]), "mpcqp_set_pairing")
+        self.pairing = mode
 
     def _device_input(self, a, shape, name):
         torch = self._torch

@@ -35,7 +35,7 @@ def test_library_exports_every_header_symbol():
         assert hasattr(handle, name), f"{name} declared in include/mpcqp.h but not exported"
     assert set(decls) == set(_lib_mod.exported_symbols())
     L = _lib_mod.lib()
-    assert L.mpcqp_version() == _lib_mod.ABI_VERSION == 7
+    assert L.mpcqp_version() == _lib_mod.ABI_VERSION == 8
     assert L.mpcqp_num_rows(20) == 101
     assert L.mpcqp_model_stride(20) % 8 == 0
 
@@ -290,10 +290,17 @@ def test_solver_kernel_resources():
     if not path.exists():
         pytest.skip("library not built in this tree (build() writes the resource record)")
     rec = json.loads(path.read_text())
-    res = {int(k): v for k, v in rec.items() if not k.startswith("loop:")}
+    res = {int(k): v for k, v in rec.items() if ":" not in k}
     loops = {int(k.split(":")[1]): v for k, v in rec.items() if k.startswith("loop:")}
+    pairs = {k: v for k, v in rec.items() if k.startswith(("pair:", "loop_pair:"))}
     assert sorted(res) == list(range(1, 33))
     assert sorted(loops) == list(range(1, 33))
+    # two QPs (vehicles) per wave, N <= 15: still 2 waves per SIMD, two LDS blocks per workgroup
+    assert sorted(pairs) == sorted([f"pair:{N}" for N in range(1, 16)] + [f"loop_pair:{N}" for N in range(1, 16)])
+    for k, r in pairs.items():
+        assert r["Occupancy"] >= 2 and r["AGPRs"] == 0, (k, r)
+        assert r["ScratchSize"] <= (0 if k.startswith("pair:") else 512), (k, r)
+        assert r["LDS"] <= 160 * 1024 // 8, (k, r)
     for N, r in loops.items():
         # the fused closed loop (k_fleet_loop<N>) runs the same solver at 2 waves per SIMD; values
         # live across the steps (loop state, output pointers) spill at the step boundary only

@@ -30,6 +30,8 @@ def main() -> None:
     ap.add_argument("--horizon", type=int, default=15)
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--fused", action="store_true", help="mpcqp_fleet_loop: one launch for the whole loop")
+    ap.add_argument("--pairing", default="auto", choices=["auto", "on", "off"],
+                    help="two vehicles per wave for N <= 15 (mpcqp_set_pairing)")
     a = ap.parse_args()
     import torch
 
@@ -44,7 +46,8 @@ def main() -> None:
     for V in a.vehicles:
         paths, starts, goals = scenarios.fleet5(V)
         mpc = MPCConfig(horizon=a.horizon, sim_steps=a.steps)
-        ft = FleetTracker(mpc, map_resolution=0.8, max_vehicles=V, max_ref_len=160, device=dev, fused=a.fused)
+        ft = FleetTracker(mpc, map_resolution=0.8, max_vehicles=V, max_ref_len=160, device=dev, fused=a.fused,
+                          pairing=a.pairing)
         best = None
         for r in range(a.reps + 1):
             torch.cuda.synchronize()
