@@ -234,10 +234,17 @@ __device__ __forceinline__ double row_bc(double v) {
   return __hiloint2double(hi, lo);
 }
 
+// Every result that crosses lanes is pinned (an empty asm volatile) where it is computed: the
+// compiler turns a lane-dependent select of a DPP result (the half-boundary cuts below) into a
+// branch and sinks the DPP into it, where its source lanes are masked off and read as 0.
 template <>
 struct Lanes<true> {
   static constexpr int kLanes = 32;
   __device__ __forceinline__ static int hl() { return (int)threadIdx.x & 31; }  // lane within the half
+  __device__ __forceinline__ static double pin(double v) {
+    asm volatile("" : "+v"(v));
+    return v;
+  }
   // w[c] lane l = v[16c + (l & 15)] of l's own half (c = 0, 1): one permlane16 swap per word
   template <int NW>
   __device__ __forceinline__ static void vbcast(double v, double w[4]) {
@@ -254,9 +261,9 @@ struct Lanes<true> {
   __device__ __forceinline__ static double read(double v) {
     double w[4];
     vbcast<2>(v, w);
-    return row_bc<K % 16>(w[K / 16]);
+    return pin(row_bc<K % 16>(w[K / 16]));
   }
-  __device__ __forceinline__ static double readv(double v, int l) { return __shfl(v, l, 32); }
+  __device__ __forceinline__ static double readv(double v, int l) { return pin(__shfl(v, l, 32)); }
   __device__ __forceinline__ static int uniform(int l) { return l; }
   // inclusive scan within the rows, then rows 1 / 3 take rows 0 / 2's total: lane 31 / 63 = the sum
   __device__ __forceinline__ static double scan(double v, int lane) {
@@ -266,7 +273,7 @@ struct Lanes<true> {
     v += dpp<kRowShr4>(v);
     v += dpp<kRowShr8>(v);
     v += dpp_rows<kRowBcast15, 0xa>(v);
-    return v;
+    return pin(v);
   }
   __device__ __forceinline__ static double sum(double v) { return read<31>(scan(v, 0)); }
   __device__ __forceinline__ static double max(double v) {  // v >= 0
@@ -283,12 +290,21 @@ struct Lanes<true> {
   }
   __device__ __forceinline__ static bool any(bool b) { return ballot(b) != 0ull; }
   // wave shifts, cut at the half boundary (what crosses it reads as 0, as past the wave's ends)
-  __device__ __forceinline__ static double shr2(double v) { return hl() >= 2 ? ::shr2(v) : 0.0; }
-  __device__ __forceinline__ static double shl2(double v) { return hl() < 30 ? ::shl2(v) : 0.0; }
+  __device__ __forceinline__ static double shr2(double v) {
+    const double d = pin(::shr2(v));
+    return hl() >= 2 ? d : 0.0;
+  }
+  __device__ __forceinline__ static double shl2(double v) {
+    const double d = pin(::shl2(v));
+    return hl() < 30 ? d : 0.0;
+  }
   __device__ __forceinline__ static double shr4(double v) { return shr2(shr2(v)); }
   __device__ __forceinline__ static double shl4(double v) { return shl2(shl2(v)); }
-  __device__ __forceinline__ static double shr1(double v) { return hl() >= 1 ? dpp<kWaveShr1>(v) : 0.0; }
-  __device__ __forceinline__ static double shfl(double v, int src) { return __shfl(v, src, 32); }
+  __device__ __forceinline__ static double shr1(double v) {
+    const double d = pin(dpp<kWaveShr1>(v));
+    return hl() >= 1 ? d : 0.0;
+  }
+  __device__ __forceinline__ static double shfl(double v, int src) { return pin(__shfl(v, src, 32)); }
 };
 
 // compile-time loop: f(std::integral_constant<int, I>) for I in [B, E)

@@ -302,7 +302,7 @@ struct Ctx {
       double d, w[4];
       if constexpr (Pair) {  // the half's lane k, from its broadcast row
         vbcast(r[k], w);
-        d = row_bc<k % 16>(w[k / 16]);
+        d = LN::pin(row_bc<k % 16>(w[k / 16]));
       } else {
         d = readlane(r[k], k);
         vbcast(r[k], w);
