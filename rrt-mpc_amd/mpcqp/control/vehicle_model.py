@@ -22,15 +22,19 @@ def f_discrete(x: State, u: Control, dt: float, wheelbase_px: float) -> State:
     The same IEEE operations in the same order as the reference.  cos / sin of one float64 are
     numpy's libm calls, so ``math.cos`` / ``math.sin`` return the same bits (a plain call instead of
     a ufunc dispatch: this runs once per closed-loop step); ``np.tan`` is numpy's own SIMD kernel,
-    which differs from libm's tan in the last ulp on ~0.5 % of arguments, so it stays.
+    which differs from libm's tan in the last ulp on ~0.5 % of arguments, so it stays.  The operands
+    are taken as Python floats (IEEE double arithmetic, the same bits as on numpy float64 scalars,
+    without their per-operation dispatch).
     ``tests/test_host.py`` holds the result to the reference's bit for bit (``vehicle.npz``)."""
-    xk, yk, yaw, v = x
-    a, delta = u
+    xk, yk, yaw, v = (x.tolist() if type(x) is np.ndarray else [float(t) for t in x])
+    a, delta = (u.tolist() if type(u) is np.ndarray else [float(t) for t in u])
+    dt, wheelbase_px = float(dt), float(wheelbase_px)
+    tan_d = float(np.tan(delta))
     return np.array(
         [
             xk + dt * v * math.cos(yaw),
             yk + dt * v * math.sin(yaw),
-            yaw + dt * (v / wheelbase_px) * np.tan(delta),
+            yaw + dt * (v / wheelbase_px) * tan_d,
             v + dt * a,
         ],
         dtype=float,
