@@ -54,6 +54,26 @@ def initial_state(path: Sequence, start) -> np.ndarray:
     return np.array([start[0], start[1], yaw0, 5.0], dtype=float)
 
 
+def initial_states(paths: Sequence, starts) -> np.ndarray:
+    """``initial_state`` of every vehicle, (V, 4): the first segments' headings by one elementwise
+    ``np.arctan2`` over all vehicles (the same float64 differences and ufunc as per path)."""
+    V = len(paths)
+    p01 = np.zeros((V, 2, 2))
+    many = np.zeros(V, dtype=bool)
+    for v, path in enumerate(paths):
+        if not len(path):
+            raise RuntimeError("Planner returned an empty path")
+        if len(path) > 1:
+            p01[v, 0] = path[0][0], path[0][1]
+            p01[v, 1] = path[1][0], path[1][1]
+            many[v] = True
+    out = np.empty((V, 4))
+    out[:, :2] = np.asarray(starts, dtype=float).reshape(V, 2)
+    out[:, 2] = np.where(many, np.arctan2(p01[:, 1, 1] - p01[:, 0, 1], p01[:, 1, 0] - p01[:, 0, 0]), 0.0)
+    out[:, 3] = 5.0
+    return out
+
+
 @dataclass
 class FleetResult:
     """Per-vehicle outcome of a fleet run (host copies)."""
@@ -121,7 +141,6 @@ class FleetTracker:
     def reset(self, ref_globals: Sequence[np.ndarray], states0: np.ndarray, goals: np.ndarray,
               max_steps: Optional[int] = None) -> None:
         """Load V references (each ``(M_v, 4)``, ``build_reference`` output), start states and goals."""
-        torch = self._torch
         V = len(ref_globals)
         if V > self.max_vehicles:
             raise ValueError(f"{V} vehicles exceed max_vehicles {self.max_vehicles}")
@@ -140,12 +159,26 @@ class FleetTracker:
             if r.ndim != 2 or r.shape[1] != 4:
                 raise ValueError("each reference must have shape (M, 4)")
             ref[v, : len(r)] = r
+        self._load(V, ref, lens, states0, goals, max_steps)
+
+    def _load(self, V: int, ref: Optional[np.ndarray], lens: np.ndarray, states0: np.ndarray, goals: np.ndarray,
+              max_steps: Optional[int]) -> None:
+        """The fleet's device buffers for V vehicles; ``ref`` None: the references are copied in on the
+        device afterwards (reset_device), so no host copy of them is built or uploaded."""
+        torch = self._torch
+        states0 = np.asarray(states0, dtype=float).reshape(V, 4)
+        goals = np.asarray(goals, dtype=float).reshape(V, 2)
+        max_steps = int(self.mpc.sim_steps if max_steps is None else max_steps)
+        if max_steps < 1:
+            raise ValueError("max_steps must be >= 1")
+        M = self.max_ref_len
         N = self.horizon
         dev = dict(device=self.device)
         f64 = torch.float64
         i32 = torch.int32
         b = {
-            "ref_global": torch.from_numpy(ref).to(**dev),
+            "ref_global": (torch.from_numpy(ref).to(**dev) if ref is not None
+                           else torch.zeros((max(V, 1), M, 4), dtype=f64, **dev)),
             "ref_len": torch.from_numpy(np.maximum(lens, 1) if V else np.ones(1, np.int32)).to(**dev),
             "goal": torch.from_numpy(goals if V else np.zeros((1, 2))).to(**dev),
             "state": torch.from_numpy(states0 if V else np.zeros((1, 4))).to(**dev),
@@ -178,12 +211,7 @@ class FleetTracker:
         ``device_reference=True`` builds the references with the batched GPU ``build_reference``
         (``mpcqp_build_reference``) straight into the fleet's buffers; otherwise on the host.
         Returns the host references (or ``(ref, ref_len)`` device tensors)."""
-        states = []
-        for path, start in zip(paths, starts):
-            if not len(path):
-                raise RuntimeError("Planner returned an empty path")
-            states.append(initial_state(path, start))
-        states0 = np.array(states).reshape(-1, 4)
+        states0 = initial_states(paths, starts)
         if device_reference:
             ref, ref_len = build_reference_batch(paths, self.mpc.v_px_s, self.horizon, self.mpc.dt,
                                                  device=self.device, ref_stride=self.max_ref_len)
@@ -199,13 +227,15 @@ class FleetTracker:
         ``ref_len`` (V,) int32 as produced by ``build_reference_batch``."""
         torch = self._torch
         V = int(ref.shape[0])
+        if V > self.max_vehicles:
+            raise ValueError(f"{V} vehicles exceed max_vehicles {self.max_vehicles}")
         if int(ref.shape[1]) != self.max_ref_len:
             raise ValueError(f"ref rows {int(ref.shape[1])} != max_ref_len {self.max_ref_len}")
         lens = ref_len.cpu().numpy()
         if V and (lens.min() < 1 or lens.max() > self.max_ref_len):
             raise ValueError(f"reference lengths must be in [1, {self.max_ref_len}] (build_reference_batch "
                              f"reports overflow as negative lengths)")
-        self.reset([np.zeros((1, 4))] * V, states0, goals, max_steps)
+        self._load(V, None, lens.astype(np.int32), states0, goals, max_steps)
         self._bufs["ref_global"][:V].copy_(ref)
         self._bufs["ref_len"][:V].copy_(ref_len.to(torch.int32))
 
@@ -268,4 +298,5 @@ class FleetTracker:
         self._relaxed.close()
 
 
-__all__ = ["FleetTracker", "FleetResult", "relaxed_parameters", "initial_state", "closed_loop_settings", "PHASE_NAMES"]
+__all__ = ["FleetTracker", "FleetResult", "relaxed_parameters", "initial_state", "initial_states", "closed_loop_settings",
+           "PHASE_NAMES"]

@@ -355,3 +355,17 @@ def test_three_argument_step_resolves_parameters(golden, monkeypatch):
     tracker.track(planning, maps, map_resolution=0.4, visualize=False)
     tracker.step(loop["N15_x0"][0], loop["N15_window"][0], loop["N15_u_prev"][0])
     assert seen[-1] == seen[-2] == 2.8 / 0.4
+
+
+def test_initial_states_equal_per_vehicle_initial_state():
+    """The fleet's vectorised start states (one elementwise arctan2 over all vehicles) equal
+    ``initial_state`` (control_stage.py:74-79) per vehicle bit for bit, one-point paths included."""
+    from mpcqp import scenarios
+    from mpcqp.pipeline.fleet import initial_state, initial_states
+
+    paths, starts, goals = scenarios.fleet5(512)
+    paths = list(paths) + [np.array([[3.0, 4.0]]), [(1.0, 2.0), (1.0, 2.0)], [(0.0, 0.0), (-1.0, -1e-300)]]
+    starts = np.vstack([starts, [[1.0, 1.0], [2.0, 2.0], [3.0, 3.0]]])
+    got = initial_states(paths, starts)
+    want = np.array([initial_state(p, s) for p, s in zip(paths, starts)])
+    np.testing.assert_array_equal(got, want)
