@@ -1,0 +1,52 @@
+#!/usr/bin/env python3
+"""Where FleetTracker.reset_from_plans(device_reference=True) spends its time (host start states,
+build_reference_batch, the fleet buffers), per fleet size, best of 5 after a warm call."""
+import json
+import sys
+import time
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parents[2]
+sys.path.insert(0, str(ROOT / "rrt-mpc_amd"))
+
+
+def main() -> None:
+    import torch
+
+    from mpcqp import scenarios
+    from mpcqp.config import MPCConfig
+    from mpcqp.control.ref_builder import build_reference_batch
+    from mpcqp.pipeline.fleet import FleetTracker, initial_states
+
+    out = {}
+    for V in (1024, 4096, 16384):
+        paths, starts, goals = scenarios.fleet5(V)
+        ft = FleetTracker(MPCConfig(horizon=15, sim_steps=100), map_resolution=0.8, max_vehicles=V, max_ref_len=160,
+                          device="cuda:0", fused=True)
+        best = {}
+        for rep in range(6):
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            s0 = initial_states(paths, starts)
+            t1 = time.perf_counter()
+            ref, ref_len = build_reference_batch(paths, ft.mpc.v_px_s, 15, ft.mpc.dt, device=ft.device, ref_stride=160)
+            torch.cuda.synchronize()
+            t2 = time.perf_counter()
+            ft.reset_device(ref, ref_len, s0, goals)
+            torch.cuda.synchronize()
+            t3 = time.perf_counter()
+            ft.reset_from_plans(paths, starts, goals, device_reference=True)
+            torch.cuda.synchronize()
+            t4 = time.perf_counter()
+            if rep:
+                for k, v in (("initial_states", t1 - t0), ("build_reference_batch", t2 - t1), ("reset_device", t3 - t2),
+                             ("reset_from_plans", t4 - t3)):
+                    best[k] = min(best.get(k, 1e9), v * 1e3)
+        out[f"V{V}"] = {k: round(v, 3) for k, v in best.items()}
+        ft.close()
+        print(json.dumps({f"V{V}": out[f"V{V}"]}), file=sys.stderr, flush=True)
+    print(json.dumps({"unit": "ms", **out}, indent=1))
+
+
+if __name__ == "__main__":
+    main()
