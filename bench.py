@@ -791,7 +791,11 @@ def main() -> int:
                 "nu": 2,
                 "method": method_label(ctrl._cparams),
                 "solver_settings": solver_settings(ctrl._cparams),
-                "pairing": args.pairing,
+                # two QPs per wave (mpcqp_set_pairing): only for N <= 15, AUTO past 8 waves per CU
+                "pairing": {"mode": args.pairing, "applied": bool(
+                    N <= 15 and not extra.get("reproducible", 0) and not extra.get("debug_state", 0) and (
+                        args.pairing == "on" or (args.pairing == "auto" and
+                                                 B > 8 * torch.cuda.get_device_properties(device).multi_processor_count)))},
                 "parallelism": f"dp{world} (independent contiguous shards, {'strong' if strong else 'weak'})",
             },
             "solved_fraction": solved_all / total,
