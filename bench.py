@@ -673,6 +673,9 @@ def main() -> int:
                     help="development: override a solver setting of mpcqp_params (repeatable)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline sample length (0 = skip)")
     ap.add_argument("--check-sample", type=int, default=512, help="QPs of the gathered result rank 0 checks")
+    ap.add_argument("--event-every", type=int, default=4,
+                    help="HIP event pair around every K-th timed step (the kernel time is their mean): a pair "
+                         "costs ~7 us of stream time per step it brackets (tools/diag/gpu_event_cost.sh)")
     ap.add_argument("--no-config1", action="store_true", help="skip the config-1 closed-loop line")
     ap.add_argument("--no-config5", action="store_true", help="skip the config-5 swarm line")
     ap.add_argument("--no-pipelined", action="store_true",
@@ -723,7 +726,7 @@ def main() -> int:
     fused = N < _lib.WIDE_MIN_HORIZON and not extra.get("reproducible", 0) and not extra.get("debug_state", 0)
 
     def step(k: int) -> None:
-        ev = events[k] if k >= 0 else None
+        ev = events[k] if k >= 0 and k % args.event_every == 0 else None
         if ev is not None:
             ev[0].record(stream)
         _lib.check(L.mpcqp_build(ctrl._ws, B, x0_t.data_ptr(), ref_t.data_ptr(), up_t.data_ptr(), s), "build")
@@ -736,12 +739,13 @@ def main() -> int:
             ev[2].record(stream)
 
     elapsed = timed_steps(step, args.steps, args.warmup, ctx, lambda: torch.cuda.synchronize(device))
+    timed = events[::args.event_every]
     if fused:
         k1_ms = 0.0
-        k2_ms = float(np.mean([e[0].elapsed_time(e[2]) for e in events]))
+        k2_ms = float(np.mean([e[0].elapsed_time(e[2]) for e in timed]))
     else:
-        k1_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in events]))
-        k2_ms = float(np.mean([e[1].elapsed_time(e[2]) for e in events]))
+        k1_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in timed]))
+        k2_ms = float(np.mean([e[1].elapsed_time(e[2]) for e in timed]))
 
     status = ctrl._status[:B].cpu().numpy()
     iters = ctrl._iters[:B].cpu().numpy()
@@ -801,6 +805,8 @@ def main() -> int:
             "solved_fraction": solved_all / total,
             "iters_mean": {"admm": admm_all / total, "polish": pol_all / total},
             "kernel_ms": {"mpcqp_build": k1_ms, "k_solve": k2_ms},
+            # HIP event pairs on the launch stream around every event_every-th timed step
+            "kernel_timing": {"event_pairs": len(timed), "event_every": args.event_every},
             "roofline": {
                 "bound": "fp64_valu",
                 "achieved": achieved_tf,
@@ -818,7 +824,8 @@ def main() -> int:
                 "note": "FP64 VALU roof (MI355X FP64 vector peak 78.6 TF; no MFMA is issued: f64 MFMA has "
                         "the same peak and the per-QP matrices are <= 62x62). k_solve is a latency-bound "
                         "FP64 VALU kernel. Flops = bench.qp_flops (as implemented, counted per QP from the "
-                        "kernel's iteration counters) / mean k_solve event time on the launch stream.",
+                        "kernel's iteration counters) / mean k_solve event time on the launch stream "
+                        "(event pairs around every event_every-th timed step: kernel_timing).",
             },
             "hbm_roofline": {
                 "achieved": hbm_gbs,
