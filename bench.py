@@ -655,8 +655,10 @@ def pipelined_leg(params, x0, ref, u_prev, steps: int, warmup: int, device, meth
 def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    # steady state: ~100 untimed steps bring the GPU to its sustained clocks (20 timed after 3 warm
+    # steps read ~8 % low: tools/diag/gpu_steps_warmup.sh); the whole default run still takes seconds
+    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--warmup", type=int, default=100)
     ap.add_argument("--config", default="config3", choices=sorted(DEFAULT_BATCH))
     ap.add_argument("--batch", type=int, default=0, help="QPs per GPU, weak scaling (default: the config's)")
     ap.add_argument("--global-batch", type=int, default=0,
