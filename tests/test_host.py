@@ -369,3 +369,20 @@ def test_initial_states_equal_per_vehicle_initial_state():
     got = initial_states(paths, starts)
     want = np.array([initial_state(p, s) for p, s in zip(paths, starts)])
     np.testing.assert_array_equal(got, want)
+
+
+def test_argument_checks_without_a_device():
+    """Entry points that validate their arguments before touching the device return MPCQP_E_ARG for
+    a null workspace or a bad mode, and report why (no GPU in this container)."""
+    import ctypes
+
+    _lib_mod = _binding()
+    L = _lib_mod.lib()
+    E_ARG = -1
+    assert L.mpcqp_set_pairing(None, _lib_mod.PAIR_ON) == E_ARG
+    assert b"null ws" in L.mpcqp_last_error()
+    assert L.mpcqp_solve_served(None) == E_ARG
+    assert L.mpcqp_solve_staged(None) == E_ARG
+    hin, hout = ctypes.c_void_p(), ctypes.c_void_p()
+    offs = (ctypes.c_int32 * 6)()
+    assert L.mpcqp_stage(None, ctypes.byref(hin), ctypes.byref(hout), offs) == E_ARG
