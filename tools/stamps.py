@@ -46,11 +46,14 @@ def main() -> None:
     ap.add_argument("--by", type=int, default=0, help="iteration counter ranking --worst (0 ADMM, 1 polish)")
     ap.add_argument("--batch", type=int, default=0)
     ap.add_argument("--horizon", type=int, default=0, help="the config's generator at another horizon")
+    ap.add_argument("--polish-from", type=int, default=None, help="solver setting polish_from (default: library's)")
     a = ap.parse_args()
     b = getattr(scenarios, a.config)(**({"horizon": a.horizon} if a.horizon else {}))
     x0, ref, up = b.x0, b.ref, b.u_prev
     B = a.batch or b.size
-    ctrl = BatchedMPCController(MPCConfig(horizon=b.horizon).to_parameters(0.8), max(B, b.size), device="cuda:0")
+    extra = {} if a.polish_from is None else {"polish_from": a.polish_from}
+    ctrl = BatchedMPCController(MPCConfig(horizon=b.horizon).to_parameters(0.8), max(B, b.size), device="cuda:0",
+                                **extra)
     L = _lib.lib()
     buf = (ctypes.c_ulonglong * 32)()
     ctrl.solve_batch(x0, ref, up)
