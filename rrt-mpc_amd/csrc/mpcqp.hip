@@ -209,9 +209,7 @@ bool use_pairs(const mpcqp_ws* ws, int count) {
   if (ws->pairing == MPCQP_PAIR_OFF) return false;
   // auto: once the QPs outnumber the wave slots (2 per SIMD): below that every QP has a wave of its
   // own, and pairing would only make each wave wait for the slower of its two QPs
-  int cus = 0;
-  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ws->device) != hipSuccess) cus = 0;
-  return cus > 0 && count > 8 * cus;
+  return ws->cus > 0 && count > 8 * ws->cus;
 }
 fleet_loop_t fleet_looper(const mpcqp_params& p) {
   if (wide_solve(p) || p.debug_state || p.horizon < 1 || p.horizon >= MPCQP_WIDE_MIN_HORIZON) return nullptr;
@@ -255,6 +253,7 @@ int mpcqp_create(const mpcqp_params* p, int max_batch, int device, mpcqp_ws** ws
   w->serve_seq = 0;
   w->serve_live = false;
   w->pairing = MPCQP_PAIR_AUTO;
+  if (hipDeviceGetAttribute(&w->cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess) w->cus = 0;
   e = hipMalloc(&w->dparams, 2 * sizeof(mpcqp_params));
   if (e == hipSuccess) e = hipMalloc(&w->dorder, sizeof(int32_t) * (size_t)max_batch);
   if (e != hipSuccess) {

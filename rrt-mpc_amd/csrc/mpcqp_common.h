@@ -498,6 +498,7 @@ struct mpcqp_ws {
   std::chrono::steady_clock::time_point serve_last;  // the last completed request (host clock)
   // two QPs per wave for N <= 15 (MPCQP_PAIR_*, mpcqp_set_pairing)
   int pairing;
+  int cus;  // the device's compute units (queried once at mpcqp_create; 0 if unknown)
 };
 
 namespace mpcqp {

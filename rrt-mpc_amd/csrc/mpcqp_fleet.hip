@@ -274,9 +274,7 @@ int enqueue_fleet_loop(mpcqp_ws* nominal, mpcqp_ws* relaxed, const mpcqp_fleet* 
   LoopTrigger tro = tr;
   // longest first only when the vehicles outnumber the wave slots (2 per SIMD): with every vehicle
   // resident at once the order only changes which vehicles share a SIMD (measured: no gain)
-  int cus = 0;
-  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, nominal->device) != hipSuccess) cus = 0;
-  if (cus > 0 && f->vehicles > 8 * cus) {
+  if (nominal->cus > 0 && f->vehicles > 8 * nominal->cus) {
     hipLaunchKernelGGL(k_fleet_order, dim3(1), dim3(kOrderBuckets), 0, s, *f, nominal->dorder);
     tro.order = nominal->dorder;
   }
