@@ -189,6 +189,27 @@ __device__ __forceinline__ void bcast(double v, double w[4]) {
   if constexpr (NW == 3) asm volatile("s_nop 1" : "+v"(w[0]), "+v"(w[1]), "+v"(w[2]));
   if constexpr (NW == 4) asm volatile("s_nop 1" : "+v"(w[0]), "+v"(w[1]), "+v"(w[2]), "+v"(w[3]));
 }
+// The same for a vector that lives in the lanes of rows 0-1 of each half (n <= 32 in the whole-wave
+// layout, n <= 30 in a half): one permlane16 swap per word puts row 0 / row 1 of each half into both
+// of its rows (w[0] / w[1]); with n <= 16 (NW = 1) row 0 is already where its lanes read it, and no
+// lane moves at all (whole-wave layout only).  The lanes of the other rows read their own rows'
+// values there: padding, which the callers keep finite (exact zeros).
+template <int NW>
+__device__ __forceinline__ void bcast_rows01(double v, double w[4]) {
+  static_assert(NW <= 2, "two 16-lane rows");
+  if constexpr (NW == 1) {
+    w[0] = v;
+    asm volatile("s_nop 1" : "+v"(w[0]));
+  } else {
+    const int lo = __double2loint(v), hi = __double2hiint(v);
+    const auto l16 = __builtin_amdgcn_permlane16_swap(lo, lo, false, false);  // rows {0,0,2,2} / {1,1,3,3}
+    const auto h16 = __builtin_amdgcn_permlane16_swap(hi, hi, false, false);
+    w[0] = __hiloint2double(h16[0], l16[0]);
+    w[1] = __hiloint2double(h16[1], l16[1]);
+    // DPP reads of a VGPR need two wait states after its VALU write; tie the pad to w
+    asm volatile("s_nop 1" : "+v"(w[0]), "+v"(w[1]));
+  }
+}
 // acc += w[lane 16*row + L] * m   (one v_fmac_f64_dpp)
 template <int L>
 __device__ __forceinline__ void fmac_bc(double& acc, double w, double m) {
@@ -208,7 +229,12 @@ template <>
 struct Lanes<false> {
   static constexpr int kLanes = kWave;
   template <int NW>
-  __device__ __forceinline__ static void vbcast(double v, double w[4]) { bcast<NW>(v, w); }
+  __device__ __forceinline__ static void vbcast(double v, double w[4]) {
+    if constexpr (NW <= 2)
+      bcast_rows01<NW>(v, w);  // rows 2-3 are padding: no permlane32 stage
+    else
+      bcast<NW>(v, w);
+  }
   template <int K>
   __device__ __forceinline__ static double read(double v) { return readlane(v, K); }
   __device__ __forceinline__ static double readv(double v, int l) { return readlane(v, l); }
@@ -245,22 +271,17 @@ struct Lanes<true> {
     asm volatile("" : "+v"(v));
     return v;
   }
-  // w[c] lane l = v[16c + (l & 15)] of l's own half (c = 0, 1): one permlane16 swap per word
+  // w[c] lane l = v[16c + (l & 15)] of l's own half (c = 0, 1): one permlane16 swap per word, also
+  // at NW = 1 (the sweep reads its pivot from w in every lane of the half)
   template <int NW>
   __device__ __forceinline__ static void vbcast(double v, double w[4]) {
     static_assert(NW <= 2, "a half holds 32 lanes");
-    const int lo = __double2loint(v), hi = __double2hiint(v);
-    const auto l16 = __builtin_amdgcn_permlane16_swap(lo, lo, false, false);  // rows {0,0,2,2} / {1,1,3,3}
-    const auto h16 = __builtin_amdgcn_permlane16_swap(hi, hi, false, false);
-    w[0] = __hiloint2double(h16[0], l16[0]);
-    w[1] = __hiloint2double(h16[1], l16[1]);
-    // DPP reads of a VGPR need two wait states after its VALU write; tie the pad to w
-    asm volatile("s_nop 1" : "+v"(w[0]), "+v"(w[1]));
+    bcast_rows01<2>(v, w);
   }
   template <int K>
   __device__ __forceinline__ static double read(double v) {
     double w[4];
-    vbcast<2>(v, w);
+    bcast_rows01<2>(v, w);
     return pin(row_bc<K % 16>(w[K / 16]));
   }
   __device__ __forceinline__ static double readv(double v, int l) { return pin(__shfl(v, l, 32)); }

@@ -370,12 +370,16 @@ struct Ctx {
     }
   }
   // (A^{-1} v)_lane
-  // No lane masks: the products read lanes 0..n-1 only, and the rows of lanes >= n are exactly
-  // zero (form() writes zeros there and every update of them multiplies by a zero), so those
-  // lanes return zero by themselves.
+  // The products read lanes 0..n-1 only, and the rows of lanes >= n are exactly zero (form()
+  // writes zeros there and every update of them multiplies by a zero), so those lanes return zero
+  // by themselves as long as what they read is finite.
   __device__ __forceinline__ double inv_mul(double v) const {
     double w[4];
-    vbcast(v, w);
+    // whole wave at n <= 32: rows 2-3 read their own lanes' v (bcast_rows01), zeroed here
+    if constexpr (!Pair && kNW <= 2)
+      vbcast(act ? v : 0.0, w);
+    else
+      vbcast(v, w);
     double a[4] = {0.0, 0.0, 0.0, 0.0};
     Unroll<0, n>::run([&](auto jc) {
       constexpr int j = decltype(jc)::value;
