@@ -75,12 +75,15 @@ def test_newton_method_matches(cuda):
     _check_against_oracle(params, batch.x0, batch.ref, batch.u_prev, out, range(0, 256, 5))
 
 
-@pytest.mark.parametrize("cfg,N,B", [("config2", 20, 1024), ("config3", 10, 1024), ("config3", 24, 1024),
+@pytest.mark.parametrize("cfg,N,B", [("config2", 20, 1024), ("config3", 4, 1024), ("config3", 8, 1024),
+                                     ("config3", 10, 1024), ("config3", 16, 1024), ("config3", 24, 1024),
                                      ("config3", 31, 1024), ("config3", 32, 1024), ("config4", 30, 4096)])
 def test_iteration_indexing_bit_exact_on_product_path(cuda, cfg, N, B):
     """The product kernel (fast mode) against the C restatement on whole batches: all four counters
     (ADMM iterations, polish passes, factorizations, line-search trials), statuses and active sets
-    identical on every QP -- the north star's bit-exact iteration / active-set indexing."""
+    identical on every QP -- the north star's bit-exact iteration / active-set indexing.  N = 4 / 8 / 16
+    run the whole-wave kernel's short broadcasts (no lane moves at 2N <= 16, one permlane16 stage at
+    2N <= 32; batches below the pairing threshold)."""
     import cpu_solver
     from mpcqp import scenarios
 
