@@ -18,14 +18,29 @@ def build_reference(path, desired_speed: float, horizon: int, dt: float) -> np.n
     return xref
 
 
+class PackedPaths:
+    """Polylines packed for the device: ``pts`` (P, 2) float64, every path's points in order, and
+    ``off`` (V + 1,) int32, path ``v`` in rows ``[off[v], off[v + 1])``.  One pass over the paths,
+    shared by ``build_reference_batch`` and the fleet's start states (``fleet.initial_states``)."""
+
+    def __init__(self, paths):
+        self.arrs = [np.asarray(p, dtype=float).reshape(-1, 2) for p in paths]
+        self.V = len(self.arrs)
+        self.counts = np.array([len(a) for a in self.arrs], dtype=np.int64)
+        self.off = np.zeros(self.V + 1, dtype=np.int32)
+        self.off[1:] = np.cumsum(self.counts)
+        self.pts = np.concatenate(self.arrs) if self.V and self.off[-1] else np.zeros((1, 2))
+
+
 def build_reference_batch(paths, desired_speed: float, horizon: int, dt: float, *, device=None,
-                          ref_stride: int | None = None, stream=None):
+                          ref_stride: int | None = None, stream=None, packed: PackedPaths | None = None):
     """``build_reference`` for many paths at once on the GPU (``mpcqp_build_reference``).
 
     Returns ``(ref, ref_len)`` as device tensors: ``ref`` is ``(V, ref_stride, 4)`` float64 with
     polyline ``v``'s reference in rows ``[0, ref_len[v])`` (identical to ``build_reference`` of that
     path, up to an ulp of ``hypot``/``atan2``), ``ref_len`` is ``(V,)`` int32.  ``ref_stride``
-    defaults to an upper bound computed on the host from the path lengths.
+    defaults to an upper bound computed on the host from the path lengths.  ``packed``: the paths
+    already packed (``PackedPaths(paths)``), so the caller's pass over them is not repeated.
     """
     import ctypes
 
@@ -36,11 +51,8 @@ def build_reference_batch(paths, desired_speed: float, horizon: int, dt: float, 
     if not torch.cuda.is_available():
         raise _lib.LibraryError("build_reference_batch needs a ROCm GPU; there is no CPU fallback")
     dev = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
-    arrs = [np.asarray(p, dtype=float).reshape(-1, 2) for p in paths]
-    V = len(arrs)
-    counts = np.array([len(a) for a in arrs], dtype=np.int64)
-    off = np.zeros(V + 1, dtype=np.int32)
-    off[1:] = np.cumsum(counts)
+    pk = packed if packed is not None else PackedPaths(paths)
+    arrs, V, counts, off = pk.arrs, pk.V, pk.counts, pk.off
     max_points = int(counts.max()) if V else 0
     if max_points > _lib.REF_MAX_POINTS:
         raise ValueError(f"a path has {max_points} points; at most {_lib.REF_MAX_POINTS} are supported")
@@ -49,7 +61,7 @@ def build_reference_batch(paths, desired_speed: float, horizon: int, dt: float, 
         arc = [float(np.hypot(*np.diff(a, axis=0).T).sum()) if len(a) > 1 else 0.0 for a in arrs]
         bound = max([max(int(np.ceil(s / step)) + 2, len(a)) for s, a in zip(arc, arrs)], default=1)
         ref_stride = max(bound, horizon + 1)
-    pts = torch.from_numpy(np.concatenate(arrs) if V and off[-1] else np.zeros((1, 2))).to(dev)
+    pts = torch.from_numpy(pk.pts).to(dev)
     off_t = torch.from_numpy(off).to(dev)
     ref = torch.empty((max(V, 1), ref_stride, 4), dtype=torch.float64, device=dev)
     ref_len = torch.empty((max(V, 1),), dtype=torch.int32, device=dev)

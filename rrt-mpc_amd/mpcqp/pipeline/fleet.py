@@ -23,7 +23,7 @@ from typing import List, Optional, Sequence
 import numpy as np
 
 from .. import _lib
-from ..control.ref_builder import build_reference, build_reference_batch
+from ..control.ref_builder import PackedPaths, build_reference, build_reference_batch
 from .control_stage import TrackingResult
 
 PHASE_NAMES = {
@@ -54,22 +54,21 @@ def initial_state(path: Sequence, start) -> np.ndarray:
     return np.array([start[0], start[1], yaw0, 5.0], dtype=float)
 
 
-def initial_states(paths: Sequence, starts) -> np.ndarray:
+def initial_states(paths: Sequence, starts, packed: Optional[PackedPaths] = None) -> np.ndarray:
     """``initial_state`` of every vehicle, (V, 4): the first segments' headings by one elementwise
-    ``np.arctan2`` over all vehicles (the same float64 differences and ufunc as per path)."""
-    V = len(paths)
-    p01 = np.zeros((V, 2, 2))
-    many = np.zeros(V, dtype=bool)
-    for v, path in enumerate(paths):
-        if not len(path):
-            raise RuntimeError("Planner returned an empty path")
-        if len(path) > 1:
-            p01[v, 0] = path[0][0], path[0][1]
-            p01[v, 1] = path[1][0], path[1][1]
-            many[v] = True
+    ``np.arctan2`` over all vehicles (the same float64 differences and ufunc as per path), read
+    from the packed polylines (``packed``: the pass ``build_reference_batch`` shares)."""
+    pk = packed if packed is not None else PackedPaths(paths)
+    V = pk.V
+    if V and pk.counts.min() == 0:
+        raise RuntimeError("Planner returned an empty path")
+    many = pk.counts > 1
+    i0 = pk.off[:-1].astype(np.int64)
+    i1 = np.where(many, i0 + 1, i0)
+    p0, p1 = pk.pts[np.minimum(i0, len(pk.pts) - 1)], pk.pts[np.minimum(i1, len(pk.pts) - 1)]
     out = np.empty((V, 4))
     out[:, :2] = np.asarray(starts, dtype=float).reshape(V, 2)
-    out[:, 2] = np.where(many, np.arctan2(p01[:, 1, 1] - p01[:, 0, 1], p01[:, 1, 0] - p01[:, 0, 0]), 0.0)
+    out[:, 2] = np.where(many, np.arctan2(p1[:, 1] - p0[:, 1], p1[:, 0] - p0[:, 0]), 0.0)
     out[:, 3] = 5.0
     return out
 
@@ -211,10 +210,11 @@ class FleetTracker:
         ``device_reference=True`` builds the references with the batched GPU ``build_reference``
         (``mpcqp_build_reference``) straight into the fleet's buffers; otherwise on the host.
         Returns the host references (or ``(ref, ref_len)`` device tensors)."""
-        states0 = initial_states(paths, starts)
+        packed = PackedPaths(paths)
+        states0 = initial_states(paths, starts, packed)
         if device_reference:
             ref, ref_len = build_reference_batch(paths, self.mpc.v_px_s, self.horizon, self.mpc.dt,
-                                                 device=self.device, ref_stride=self.max_ref_len)
+                                                 device=self.device, ref_stride=self.max_ref_len, packed=packed)
             self.reset_device(ref, ref_len, states0, goals, max_steps)
             return ref, ref_len
         refs = [build_reference(path, self.mpc.v_px_s, self.horizon, self.mpc.dt) for path in paths]
