@@ -24,12 +24,29 @@ class PackedPaths:
     shared by ``build_reference_batch`` and the fleet's start states (``fleet.initial_states``)."""
 
     def __init__(self, paths):
-        self.arrs = [np.asarray(p, dtype=float).reshape(-1, 2) for p in paths]
-        self.V = len(self.arrs)
-        self.counts = np.array([len(a) for a in self.arrs], dtype=np.int64)
-        self.off = np.zeros(self.V + 1, dtype=np.int32)
+        self.V = V = len(paths)
+        pts = None
+        if V:  # one C-level concatenation of (k, 2) point arrays / lists (no per-path conversion)
+            try:
+                counts = np.fromiter(map(len, paths), dtype=np.int64, count=V)
+                cat = np.concatenate(paths, axis=0).astype(float, copy=False)
+                if cat.ndim == 2 and cat.shape == (int(counts.sum()), 2):
+                    pts = cat
+            except (ValueError, TypeError):
+                pts = None
+        if pts is None:  # ragged / empty / unusual element types: per path
+            arrs = [np.asarray(q, dtype=float).reshape(-1, 2) for q in paths]
+            counts = np.array([len(a) for a in arrs], dtype=np.int64)
+            pts = np.concatenate(arrs) if V else np.zeros((0, 2))
+        self.counts = counts if V else np.zeros(0, dtype=np.int64)
+        self.off = np.zeros(V + 1, dtype=np.int32)
         self.off[1:] = np.cumsum(self.counts)
-        self.pts = np.concatenate(self.arrs) if self.V and self.off[-1] else np.zeros((1, 2))
+        self.pts = pts if len(pts) else np.zeros((1, 2))
+
+    @property
+    def arrs(self):
+        """Path v's points as a view of ``pts``."""
+        return [self.pts[self.off[v]:self.off[v + 1]] for v in range(self.V)]
 
 
 def build_reference_batch(paths, desired_speed: float, horizon: int, dt: float, *, device=None,
@@ -52,12 +69,13 @@ def build_reference_batch(paths, desired_speed: float, horizon: int, dt: float, 
         raise _lib.LibraryError("build_reference_batch needs a ROCm GPU; there is no CPU fallback")
     dev = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
     pk = packed if packed is not None else PackedPaths(paths)
-    arrs, V, counts, off = pk.arrs, pk.V, pk.counts, pk.off
+    V, counts, off = pk.V, pk.counts, pk.off
     max_points = int(counts.max()) if V else 0
     if max_points > _lib.REF_MAX_POINTS:
         raise ValueError(f"a path has {max_points} points; at most {_lib.REF_MAX_POINTS} are supported")
     step = max(2.0, 0.8 * desired_speed * dt)
     if ref_stride is None:  # resampled rows <= ceil(arc length / step) + 1, raw rows = points
+        arrs = pk.arrs
         arc = [float(np.hypot(*np.diff(a, axis=0).T).sum()) if len(a) > 1 else 0.0 for a in arrs]
         bound = max([max(int(np.ceil(s / step)) + 2, len(a)) for s, a in zip(arc, arrs)], default=1)
         ref_stride = max(bound, horizon + 1)

@@ -371,6 +371,29 @@ def test_initial_states_equal_per_vehicle_initial_state():
     np.testing.assert_array_equal(got, want)
 
 
+def test_packed_paths_equal_per_path_packing():
+    """PackedPaths (one concatenation; the per-path fallback for ragged / empty / odd inputs) packs
+    exactly what a per-path np.asarray(...).reshape(-1, 2) packing gives."""
+    from mpcqp import scenarios
+    from mpcqp.control.ref_builder import PackedPaths
+
+    paths, _, _ = scenarios.fleet5(64)
+    cases = [list(paths), [], [np.zeros((0, 2))], [np.array([[1.0, 2.0], [3.0, 4.0]]), []],
+             [[(1, 2), (3, 4)], np.array([[5.0, 6.0]])], [np.array([[1, 2], [3, 5]])],
+             [np.array([1.0, 2.0, 3.0, 4.0]), np.array([[5.0, 6.0]])]]
+    for c in cases:
+        pk = PackedPaths(c)
+        arrs = [np.asarray(q, dtype=float).reshape(-1, 2) for q in c]
+        assert pk.V == len(c)
+        assert pk.counts.tolist() == [len(a) for a in arrs]
+        assert pk.off.tolist() == [0] + np.cumsum([len(a) for a in arrs]).astype(int).tolist()
+        if arrs and sum(len(a) for a in arrs):
+            assert pk.pts.dtype == np.float64
+            np.testing.assert_array_equal(pk.pts, np.concatenate(arrs))
+        for a, b in zip(pk.arrs, arrs):
+            np.testing.assert_array_equal(a, b)
+
+
 def test_argument_checks_without_a_device():
     """Entry points that validate their arguments before touching the device return MPCQP_E_ARG for
     a null workspace or a bad mode, and report why (no GPU in this container)."""
