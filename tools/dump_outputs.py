@@ -18,7 +18,7 @@ sys.path[:0] = [str(ROOT / "rrt-mpc_amd")]
 
 WORKLOADS = [("config2", 20, 1024), ("config3", 20, 4096), ("config4", 30, 4096), ("config3", 10, 1024),
              ("config3", 15, 1024), ("config3", 32, 512), ("config3", 40, 256), ("config3", 4, 1024),
-             ("config3", 8, 1024), ("config3", 16, 1024)]
+             ("config3", 8, 1024), ("config3", 16, 1024), ("config3", 10, 4096), ("config3", 15, 4096)]
 
 
 def dump(path: str) -> None:
