@@ -210,6 +210,46 @@ def gather_rows(ctx: DistContext, t, counts: List[int]):
     return torch.cat([p[:c] for p, c in zip(parts, counts)])
 
 
+# ------------------------------------------------------------------ launcher (--gpus N without torchrun)
+def free_port() -> int:
+    import socket
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def rank_launch_cmd(gpus: int, argv: List[str], script: Optional[str] = None, port: Optional[int] = None) -> List[str]:
+    """The command the parent runs for `bench.py --gpus N` started without torch.distributed.run: the
+    driver's own launch line (one rank per GPU, rendezvous on 127.0.0.1) around this script."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={int(gpus)}",
+            "--master-addr=127.0.0.1", f"--master-port={port or free_port()}", script or str(Path(__file__).resolve()),
+            *argv]
+
+
+def launch_ranks(gpus: int, argv: List[str], script: Optional[str] = None) -> int:
+    """Parent process of a multi-GPU run: starts `gpus` ranks (torch.distributed.run as a child; this
+    process never touches the GPU, so no rank is exec'd from a GPU-initialised process), lets rank 0's
+    JSON line through on the shared stdout, and returns non-zero when any rank failed (the launcher
+    tears the other ranks down and exits non-zero then)."""
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC only on these hosts (RCCL)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "LOCAL_WORLD_SIZE", "GROUP_RANK", "ROLE_RANK"):
+        env.pop(k, None)
+    import subprocess
+
+    return subprocess.run(rank_launch_cmd(gpus, argv, script), env=env).returncode
+
+
+def world_mismatch(gpus: int, env: Optional[Dict[str, str]] = None) -> Optional[str]:
+    """An error message when the ranks that were started disagree with --gpus, else None."""
+    env = os.environ if env is None else env
+    ws = env.get("WORLD_SIZE")
+    if ws is not None and int(ws) != int(gpus):
+        return f"--gpus {gpus} but WORLD_SIZE={ws}: launch one rank per GPU (--nproc-per-node {gpus}) or fix --gpus"
+    return None
+
+
 # ------------------------------------------------------------------ checker / CPU baseline leg
 def _cpu_model() -> str:
     try:
@@ -287,6 +327,15 @@ def cpu_baseline(params, x0, ref, u_prev, seconds: float, settings=None) -> dict
         out1 = cpu_solver.cpu_solve(params, x0[:256], ref[:256], u_prev[:256], nthreads=1, **(settings or {}))
         n1 += int((out1["status"] == 1).sum())
     dt1 = time.perf_counter() - t1
+    # every core this process may run on (SURVEY.md 8(d) "the host's cores"): a shorter slice, since
+    # on the GPU box those cores are the whole node's, shared with its other GPUs' host work
+    na, ta = 0, time.perf_counter()
+    while True:
+        outa = cpu_solver.cpu_solve(params, x0, ref, u_prev, nthreads=visible, **(settings or {}))
+        na += int((outa["status"] == 1).sum())
+        if time.perf_counter() - ta >= min(5.0, max(1.0, seconds / 2)):
+            break
+    dta = time.perf_counter() - ta
     return {
         "value": solved / dt,
         "unit": "QP/s",
@@ -295,23 +344,67 @@ def cpu_baseline(params, x0, ref, u_prev, seconds: float, settings=None) -> dict
         "threads": threads,
         "host_cores_visible": visible,
         "value_1core": n1 / dt1,
+        "value_all_cores": na / dta,
+        "threads_all_cores": visible,
         "cpu_model": _cpu_model(),
         "sample": f"{done} QPs ({done // len(x0)} passes over this rank's batch) in {dt:.1f} s on {threads} "
                   f"OpenMP threads: the host's CPU share of this GPU (OMP_NUM_THREADS; {visible} cores are "
                   f"visible to the process, shared with the node's other GPUs); C restatement of the same "
-                  f"ADMM+polish algorithm (oracle/mpcqp_cpu.c)",
+                  f"ADMM+polish algorithm (oracle/mpcqp_cpu.c); value_1core: one thread on 256 QPs; "
+                  f"value_all_cores: all {visible} visible cores on the same batch ({dta:.1f} s)",
     }
 
 
-def config5_swarm(vehicles: int = 100) -> dict:
-    """BASELINE config 5 on one GPU (the 8-GPU run shards the vehicles): a swarm of
-    `vehicles` on the default inflated grid -- batched RRT* plans, device references, the closed loop
-    with the per-step replan trigger and replanning -- through the fused swarm loop
-    (mpcqp_swarm_loop), timed end to end, and checked vehicle for vehicle against the graph-stepped
-    swarm (mpcqp_swarm_run), whose per-step operations it fuses."""
+def config5_swarm_sharded(ctx: DistContext, vehicles: int = 100) -> Optional[dict]:
+    """BASELINE config 5 on `ctx.world` GPUs: the same swarm as config5_swarm, its vehicles sharded
+    contiguously over the ranks (mpcqp.pipeline.swarm.run_swarm_sharded: every vehicle keeps its own
+    seed, so it does exactly what it does on one GPU; one all_gather_object of the per-vehicle results
+    at the end).  Timed between barriers, MAX over ranks; rank 0 then runs the whole swarm alone on its
+    own GPU and compares vehicle for vehicle.  Returns the record on rank 0, None elsewhere."""
     import torch
+    import torch.distributed as dist
+    from mpcqp.pipeline.swarm import Swarm, run_swarm_sharded, shard_vehicles
+
+    occ, starts, goals, mpc, planner = _config5_inputs(vehicles)
+    lo, hi = shard_vehicles(vehicles, ctx.world, ctx.rank)
+    sw = Swarm(occ, mpc, planner, map_resolution=0.8, max_vehicles=max(1, hi - lo), device=ctx.device,
+               replan_distance=5.5, max_replans=2, fused=True)
+    sw.run(starts[:4], goals[:4], seeds=np.arange(4), sim_steps=5)  # warm
+    torch.cuda.synchronize(ctx.device)
+    ctx.barrier()
+    t0 = time.perf_counter()
+    res = run_swarm_sharded(sw.run, starts, goals, np.arange(vehicles), rank=ctx.rank, world=ctx.world,
+                            all_gather_object=dist.all_gather_object, check_every=50)
+    torch.cuda.synchronize(ctx.device)
+    ctx.barrier()
+    T, _ = reduce_stats(ctx, time.perf_counter() - t0, [0.0])
+    if ctx.rank != 0:
+        return None
+    one = Swarm(occ, mpc, planner, map_resolution=0.8, max_vehicles=vehicles, device=ctx.device,
+                replan_distance=5.5, max_replans=2, fused=True)
+    ref = one.run(starts, goals, seeds=np.arange(vehicles), check_every=50)
+    same = (np.array_equal(res.steps, ref.steps) and np.array_equal(res.phase, ref.phase)
+            and np.array_equal(res.replans, ref.replans)
+            and all(np.array_equal(a, b) for a, b in zip(res.states, ref.states)))
+    vsteps = int(res.steps.sum())
+    return {
+        "workload": f"config5: {vehicles} vehicles sharded over {ctx.world} ranks ({shard_vehicles(vehicles, ctx.world, 0)[1]} "
+                    f"on rank 0), default inflated grid, N=15, replan trigger 5.5 px, <= 2 replans per vehicle",
+        "n_gpus": ctx.world,
+        "seconds": T,
+        "vehicle_steps": vsteps,
+        "vehicle_steps_per_s": vsteps / T,
+        "goal_reached": int((res.phase == 1).sum()),
+        "replans": int(res.replans.sum()),
+        "identical_to_one_gpu_swarm": bool(same),
+        "note": "end to end per rank (planning, references, tracking with replanning; fused loop) plus the "
+                "all_gather_object of the results, between barriers, MAX over ranks; compared vehicle for "
+                "vehicle with the whole swarm run on rank 0's GPU alone",
+    }
+
+
+def _config5_inputs(vehicles: int):
     from mpcqp.config import MPCConfig
-    from mpcqp.pipeline.swarm import Swarm
     from mpcqp.planning.rrt_star import default_planner_parameters
 
     occ = np.load(ROOT / "rrt-mpc_amd" / "mpcqp" / "data" / "default_plan.npz")["occupancy"]
@@ -323,11 +416,22 @@ def config5_swarm(vehicles: int = 100) -> dict:
         if np.hypot(*(a - b)) > 30:
             starts.append(a[::-1].astype(float))
             goals.append(b[::-1].astype(float))
-    starts, goals = np.array(starts), np.array(goals)
-    mpc = MPCConfig(horizon=15, sim_steps=300)
+    return occ, np.array(starts), np.array(goals), MPCConfig(horizon=15, sim_steps=300), default_planner_parameters()
+
+
+def config5_swarm(vehicles: int = 100) -> dict:
+    """BASELINE config 5 on one GPU (the N-GPU run shards the vehicles: config5_swarm_sharded): a swarm of
+    `vehicles` on the default inflated grid -- batched RRT* plans, device references, the closed loop
+    with the per-step replan trigger and replanning -- through the fused swarm loop
+    (mpcqp_swarm_loop), timed end to end, and checked vehicle for vehicle against the graph-stepped
+    swarm (mpcqp_swarm_run), whose per-step operations it fuses."""
+    import torch
+    from mpcqp.pipeline.swarm import Swarm
+
+    occ, starts, goals, mpc, planner = _config5_inputs(vehicles)
     runs = {}
     for fused in (True, False):
-        sw = Swarm(occ, mpc, default_planner_parameters(), map_resolution=0.8, max_vehicles=vehicles,
+        sw = Swarm(occ, mpc, planner, map_resolution=0.8, max_vehicles=vehicles,
                    device="cuda:0", replan_distance=5.5, max_replans=2, fused=fused)
         sw.run(starts[:4], goals[:4], seeds=np.arange(4), sim_steps=5)  # warm
         torch.cuda.synchronize()
@@ -484,16 +588,11 @@ def settings_key(cparams) -> str:
 
 
 def lib_key() -> str:
-    """Fingerprint of the kernel library the run loads (keys the committed PMC passes)."""
-    import hashlib
-
+    """Fingerprint of the kernel library the run loads (keys the committed PMC passes): its build id,
+    the hash of the sources it was built from (mpcqp_build_id, __graft_entry__.source_hash)."""
     from mpcqp import _lib
 
-    h = hashlib.sha256()
-    with open(_lib.LIB_PATH, "rb") as f:
-        for chunk in iter(lambda: f.read(1 << 20), b""):
-            h.update(chunk)
-    return h.hexdigest()[:16]
+    return _lib.build_id()[:16]
 
 
 def method_label(cparams) -> str:
@@ -651,6 +750,71 @@ def pipelined_leg(params, x0, ref, u_prev, steps: int, warmup: int, device, meth
             c.close()
 
 
+def strong_leg(ctx: DistContext, steps: int, warmup: int, method: str, extra: dict, total: int = 16384,
+               config: str = "config4", check: int = 64) -> Optional[dict]:
+    """BASELINE config 4 as strong scaling: a fixed global batch (16384 Monte-Carlo start poses, N = 30)
+    split contiguously over the ranks, timed like the headline (warmup, then `steps` steps between
+    barriers + device syncs, MAX over ranks), the per-QP results gathered to rank 0 afterwards and
+    spot-checked there.  Every world size runs it, N = 1 included, so the driver's per-N lines carry
+    the strong-scaling curve beside the weak headline.  Returns the record on rank 0."""
+    import torch
+
+    from mpcqp import _lib
+    from mpcqp.config import MPCConfig
+    from mpcqp.control.mpc_controller import BatchedMPCController
+
+    batch = make_global_batch(config, total)
+    lo, hi = shard_bounds(total, ctx.world, ctx.rank)
+    counts = shard_counts(total, ctx.world)
+    B = hi - lo
+    params = MPCConfig(horizon=batch.horizon).to_parameters(0.8)
+    ctrl = BatchedMPCController(params, max(1, B), device=ctx.device, method=method, **extra)
+    try:
+        x0_t, ref_t, up_t = (torch.from_numpy(a[lo:hi]).to(ctx.device) for a in (batch.x0, batch.ref, batch.u_prev))
+        L = _lib.lib()
+        stream = torch.cuda.current_stream(ctx.device)
+        s = ctypes.c_void_p(stream.cuda_stream)
+
+        def step(k: int) -> None:
+            _lib.check(L.mpcqp_build(ctrl._ws, B, x0_t.data_ptr(), ref_t.data_ptr(), up_t.data_ptr(), s), "build")
+            _lib.check(L.mpcqp_solve(ctrl._ws, B, ctrl._u0.data_ptr(), ctrl._X.data_ptr(), ctrl._U.data_ptr(),
+                                     ctrl._status.data_ptr(), ctrl._iters.data_ptr(), ctrl._active.data_ptr(), s),
+                       "solve")
+
+        elapsed = timed_steps(step, steps, warmup, ctx, lambda: torch.cuda.synchronize(ctx.device))
+        status = ctrl._status[:B]
+        T, (solved,) = reduce_stats(ctx, elapsed, [float((status == 1).sum().item())])
+        g = {k: gather_rows(ctx, t[:B], counts).cpu().numpy() for k, t in
+             (("status", ctrl._status), ("U", ctrl._U), ("active", ctrl._active))}
+        if ctx.rank != 0:
+            return None
+        out = {
+            "metric": f"MPC QP solves/s (horizon={batch.horizon}, global batch={total}), strong scaling",
+            "workload": batch.name,
+            "value": solved * steps / T,
+            "unit": "QP/s",
+            "n_gpus": ctx.world,
+            "scaling": "strong",
+            "global_batch": total,
+            "batch_per_gpu": counts,
+            "ms_per_step": 1e3 * T / steps,
+            "steps": steps,
+            "warmup": warmup,
+            "solved_fraction": solved / total,
+            "note": "BASELINE config 4: the fixed global batch split over the ranks, the same timing rule as the "
+                    "headline (barriers + device syncs around the K steps, MAX over ranks); no data-path "
+                    "collective, one gather of the results after timing",
+        }
+        if check > 0:
+            idx = np.unique(np.linspace(0, total - 1, min(total, check)).astype(int))
+            out["rel_err"] = spot_check(params, batch.x0, batch.ref, batch.u_prev, g["U"], g["active"], g["status"],
+                                        idx, settings=extra)
+            out["rel_err"]["gathered_qps"] = int(len(g["status"]))
+        return out
+    finally:
+        ctrl.close()
+
+
 # ------------------------------------------------------------------ main
 def main() -> int:
     ap = argparse.ArgumentParser()
@@ -680,6 +844,8 @@ def main() -> int:
                          "costs ~7 us of stream time per step it brackets (tools/diag/gpu_event_cost.sh)")
     ap.add_argument("--no-config1", action="store_true", help="skip the config-1 closed-loop line")
     ap.add_argument("--no-config5", action="store_true", help="skip the config-5 swarm line")
+    ap.add_argument("--no-strong", action="store_true",
+                    help="skip the config-4 strong-scaling leg (16384 QPs, N = 30, split over the ranks)")
     ap.add_argument("--no-pipelined", action="store_true",
                     help="skip the leg that overlaps consecutive batches on two streams")
     ap.add_argument("--no-osqp-settings", action="store_true",
@@ -688,6 +854,13 @@ def main() -> int:
                     help="torch.distributed backend for N > 1 (nccl = RCCL; gloo only to rehearse "
                          "several ranks on one GPU)")
     args = ap.parse_args()
+    bad = world_mismatch(args.gpus)
+    if bad:
+        print(f"bench.py: {bad}", file=sys.stderr)
+        return 2
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # `bench.py --gpus N` on its own: start the N ranks (before anything touches the GPU)
+        return launch_ranks(args.gpus, sys.argv[1:])
 
     import torch
 
@@ -803,6 +976,7 @@ def main() -> int:
                         args.pairing == "on" or (args.pairing == "auto" and
                                                  B > 8 * torch.cuda.get_device_properties(device).multi_processor_count)))},
                 "parallelism": f"dp{world} (independent contiguous shards, {'strong' if strong else 'weak'})",
+                "build_id": _lib.build_id(),
             },
             "solved_fraction": solved_all / total,
             "iters_mean": {"admm": admm_all / total, "polish": pol_all / total},
@@ -845,6 +1019,18 @@ def main() -> int:
                                         g["status"], idx, g["iters"], settings=extra)
             out["rel_err"]["gathered_qps"] = int(len(g["status"]))
             out["rel_err"]["gathered_solved"] = int((g["status"] == 1).sum())
+    # legs every rank takes part in (collectives inside): config 4 as strong scaling at every world size,
+    # config 5 sharded by vehicle past one GPU
+    headline = args.config == "config3" and not args.horizon and not strong
+    if headline and not args.no_strong:
+        rec = strong_leg(ctx, args.steps, args.warmup, args.method, extra)
+        if rank == 0:
+            out["strong_config4"] = rec
+    if headline and world > 1 and not args.no_config5:
+        rec = config5_swarm_sharded(ctx)
+        if rank == 0:
+            out["config5"] = rec
+    if rank == 0:
         if world == 1 and not args.no_pipelined:
             out["pipelined"] = pipelined_leg(params, x0, ref, u_prev, args.steps, args.warmup, device, args.method,
                                              extra, ctrl._U[:B])

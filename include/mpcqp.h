@@ -131,6 +131,10 @@ typedef struct mpcqp_ws mpcqp_ws;
 /* ABI version (MPCQP_ABI_VERSION). */
 int mpcqp_version(void);
 
+/* Build id of this library: a hash of its sources and compile flags (__graft_entry__.source_hash),
+ * compiled in by build(), which rebuilds whenever the sources' hash differs from it.  32 hex digits. */
+const char* mpcqp_build_id(void);
+
 /* Thread-local description of the last error ("" if none). */
 const char* mpcqp_last_error(void);
 

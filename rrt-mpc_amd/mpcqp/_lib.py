@@ -231,6 +231,7 @@ _lib: Optional[ctypes.CDLL] = None
 _SYMBOLS = {
     "mpcqp_version": ([], ctypes.c_int),
     "mpcqp_last_error": ([], ctypes.c_char_p),
+    "mpcqp_build_id": ([], ctypes.c_char_p),
     "mpcqp_num_rows": ([ctypes.c_int], ctypes.c_int),
     "mpcqp_create": ([ctypes.POINTER(MpcqpParams), ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_void_p)],
                      ctypes.c_int),
@@ -275,6 +276,11 @@ _SYMBOLS = {
     "mpcqp_solve_served": ([ctypes.c_void_p], ctypes.c_int),
     "mpcqp_set_pairing": ([ctypes.c_void_p, ctypes.c_int], ctypes.c_int),
 }
+
+
+def build_id() -> str:
+    """mpcqp_build_id() of the loaded library."""
+    return lib().mpcqp_build_id().decode()
 
 
 def exported_symbols():

@@ -25,6 +25,17 @@ def _binding():
     return _lib
 
 
+def test_library_build_id_matches_the_sources():
+    """The shipped libmpcqp.so is the one HEAD's sources build: its compiled-in build id equals the
+    hash of the sources and the compile recipe (a stale library fails here, whatever its mtime)."""
+    import __graft_entry__ as g
+
+    _lib_mod = _binding()
+    want = g.source_hash()
+    assert g.library_build_id() == want, "libmpcqp.so is stale: rebuild with __graft_entry__.build()"
+    assert _lib_mod.lib().mpcqp_build_id().decode() == want
+
+
 def test_library_exports_every_header_symbol():
     _lib_mod = _binding()
     text = HEADER.read_text()
