@@ -273,6 +273,23 @@ def host_threads() -> Tuple[int, int]:
     return threads, visible
 
 
+def cgroup_cpu_quota() -> Optional[float]:
+    """Cores this process's cgroup may use (cpu.max quota / period), None when unlimited or unknown: on
+    the GPU box the affinity mask shows the whole node while the job's CPU share is far smaller."""
+    for f in ("/sys/fs/cgroup/cpu.max",):
+        try:
+            q, per = open(f).read().split()[:2]
+            return None if q == "max" else int(q) / int(per)
+        except (OSError, ValueError):
+            pass
+    try:
+        q = int(open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read())
+        per = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+        return None if q <= 0 else q / per
+    except (OSError, ValueError):
+        return None
+
+
 def spot_check(params, x0, ref, u_prev, U, active, status, idx, iters=None, settings=None) -> dict:
     """Checker: the GPU solutions of QPs `idx` against the C restatement, whose polish ends at the
     exact optimum of the QP (strictly convex: the same optimum OSQP+polish returns in the
@@ -346,12 +363,14 @@ def cpu_baseline(params, x0, ref, u_prev, seconds: float, settings=None) -> dict
         "value_1core": n1 / dt1,
         "value_all_cores": na / dta,
         "threads_all_cores": visible,
+        "cgroup_cpu_quota_cores": cgroup_cpu_quota(),
         "cpu_model": _cpu_model(),
         "sample": f"{done} QPs ({done // len(x0)} passes over this rank's batch) in {dt:.1f} s on {threads} "
                   f"OpenMP threads: the host's CPU share of this GPU (OMP_NUM_THREADS; {visible} cores are "
                   f"visible to the process, shared with the node's other GPUs); C restatement of the same "
                   f"ADMM+polish algorithm (oracle/mpcqp_cpu.c); value_1core: one thread on 256 QPs; "
-                  f"value_all_cores: all {visible} visible cores on the same batch ({dta:.1f} s)",
+                  f"value_all_cores: all {visible} visible cores on the same batch ({dta:.1f} s; above the "
+                  f"cgroup's CPU quota, cgroup_cpu_quota_cores, the threads oversubscribe it)",
     }
 
 

@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define MPCQP_ABI_VERSION 8
+#define MPCQP_ABI_VERSION 9
 
 /* error codes (function return values) */
 #define MPCQP_OK 0
@@ -200,9 +200,13 @@ int mpcqp_solve_staged(mpcqp_ws* ws);
  * workspace's stream that solves the staged QP each time this function raises a request in a
  * mailbox of mapped host memory, and publishes completion there (the call spins on it).  The wave
  * leaves after 2 ms without a request, at mpcqp_set_params and at mpcqp_destroy; the next call
- * starts it again.  While it is resident, a device-wide synchronisation (hipDeviceSynchronize)
- * waits for it to go idle.  Horizons without the one-wave kernel (N > 32, reproducible, debug
- * builds) run mpcqp_solve_staged. */
+ * starts it again.  One server is resident per device: a request on another workspace of the same
+ * device first stops the live one (a switch costs one stop and one launch).  The workspace's stream
+ * has the device's highest priority, so its hardware queue is not one that default-priority streams
+ * (torch's) share.  While a wave is resident, a device-wide synchronisation (hipDeviceSynchronize)
+ * waits for it to go idle.  A request unanswered for 30 s returns MPCQP_E_DEVICE and the workspace
+ * refuses later B = 1 requests.  Horizons without the one-wave kernel (N > 32, reproducible, debug
+ * builds) run mpcqp_solve_staged.  Not thread-safe per workspace (the closed loop is sequential). */
 int mpcqp_solve_served(mpcqp_ws* ws);
 
 /* Two QPs per wave for horizons N <= 15 (2N <= 30 variables: a one-wave QP leaves half its lanes on
@@ -447,6 +451,11 @@ int mpcqp_ws_state_stride(const mpcqp_ws* ws);
 /* Test hook: applies the kernels' 64-lane wavefront primitives (DPP prefix/suffix scans,
  * reductions, lane shifts) to in[64] -> out[10 x 64] on the device. */
 int mpcqp_debug_wave_ops(const double* in, double* out, void* stream);
+
+/* Test hook for the B = 1 server's failure paths: mode 1 refuses the next server launch
+ * (MPCQP_E_HIP), mode 2 makes the live wave leave without telling the host (the next request finds it
+ * gone and relaunches it), mode 3 returns 1 while a server is believed resident, else 0. */
+int mpcqp_debug_serve_fault(mpcqp_ws* ws, int mode);
 
 /* Diagnostic builds only (-DMPCQP_STAMPS; the measured library returns MPCQP_E_ARG):
  * per-phase s_memtime cycle sums over all waves since the last reset. */

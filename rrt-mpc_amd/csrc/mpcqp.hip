@@ -15,6 +15,7 @@
 #include "mpcqp_build.h"
 
 #include <chrono>
+#include <mutex>
 #ifdef MPCQP_ONLY_N
 #include "mpcqp_solve.h"  // development builds: one horizon, one translation unit
 #endif
@@ -252,6 +253,8 @@ int mpcqp_create(const mpcqp_params* p, int max_batch, int device, mpcqp_ws** ws
   w->serve_box = w->serve_box_d = nullptr;
   w->serve_seq = 0;
   w->serve_live = false;
+  w->serve_broken = false;
+  w->serve_fault = 0;
   w->pairing = MPCQP_PAIR_AUTO;
   if (hipDeviceGetAttribute(&w->cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess) w->cus = 0;
   e = hipMalloc(&w->dparams, 2 * sizeof(mpcqp_params));
@@ -292,12 +295,12 @@ int mpcqp_set_params(mpcqp_ws* ws, const mpcqp_params* p) {
 void mpcqp_destroy(mpcqp_ws* ws) {
   if (!ws) return;
   (void)hipSetDevice(ws->device);
+  serve_stop(ws);  // first: the frees below synchronise the device, which waits for a resident wave
+  if (ws->stage_stream) (void)hipStreamSynchronize(ws->stage_stream);
   (void)hipFree(ws->model);
   (void)hipFree(ws->state);
   (void)hipFree(ws->dparams);
   (void)hipFree(ws->dorder);
-  serve_stop(ws);
-  if (ws->stage_stream) (void)hipStreamSynchronize(ws->stage_stream);
   if (ws->serve_box) (void)hipHostFree(ws->serve_box);
   if (ws->stage_in) (void)hipHostFree(ws->stage_in);
   if (ws->stage_out) (void)hipHostFree(ws->stage_out);
@@ -386,7 +389,12 @@ int mpcqp_stage(mpcqp_ws* ws, double** in, void** out, int32_t offsets[6]) {
     if (e == hipSuccess) e = hipHostMalloc((void**)&hout, (size_t)off[6], fl);
     if (e == hipSuccess) e = hipHostGetDevicePointer(&din, hin, 0);
     if (e == hipSuccess) e = hipHostGetDevicePointer(&dout, hout, 0);
-    if (e == hipSuccess) e = hipStreamCreateWithFlags(&st, hipStreamNonBlocking);
+    // the highest stream priority: the runtime gives each priority its own hardware queues, so the
+    // resident server wave of mpcqp_solve_served never sits in a queue that torch's (default-priority)
+    // streams share -- a queued packet behind a resident kernel waits until it leaves
+    int least = 0, greatest = 0;
+    if (e == hipSuccess) e = hipDeviceGetStreamPriorityRange(&least, &greatest);
+    if (e == hipSuccess) e = hipStreamCreateWithPriority(&st, hipStreamNonBlocking, greatest);
     if (cur >= 0 && cur != ws->device) (void)hipSetDevice(cur);
     if (e != hipSuccess) {
       if (hin) (void)hipHostFree(hin);
@@ -428,9 +436,21 @@ int mpcqp_solve_staged(mpcqp_ws* ws) {
   return MPCQP_OK;
 }
 
+// One resident server wave per device: a workspace that raises a request first stops another
+// workspace's live server on its device (the drop-in alternates nominal, relaxed and scaling-10
+// workspaces), so two resident waves never hold two hardware queues and a switch costs one stop and
+// one launch.  g_server[d]: the workspace whose server may be live on device d.
+static std::mutex g_serve_mu;
+static mpcqp_ws* g_server[64] = {};
+
 // The B = 1 server (k_serve): ends a live server wave (kServeStop) and waits for it.
 static void serve_stop(mpcqp_ws* ws) {
-  if (!ws || !ws->serve_live) return;
+  if (!ws) return;
+  {
+    std::lock_guard<std::mutex> lk(g_serve_mu);
+    if (g_server[ws->device & 63] == ws) g_server[ws->device & 63] = nullptr;
+  }
+  if (!ws->serve_live) return;
   auto* box = static_cast<mpcqp::ServeBox*>(ws->serve_box);
   __atomic_store_n(&box->req, mpcqp::kServeStop, __ATOMIC_RELEASE);
   (void)hipStreamSynchronize(ws->stage_stream);
@@ -443,8 +463,17 @@ static void serve_stop(mpcqp_ws* ws) {
 int mpcqp_solve_served(mpcqp_ws* ws) {
   if (!ws) return fail(MPCQP_E_ARG, "null ws");
   if (!ws->stage_in) return fail(MPCQP_E_STATE, "mpcqp_solve_served before mpcqp_stage");
+  if (ws->serve_broken)
+    return fail(MPCQP_E_DEVICE, "B=1 server: an earlier request went unanswered; this workspace is unusable");
   const mpcqp::serve_t launch = mpcqp::server(ws->p);
   if (!launch) return mpcqp_solve_staged(ws);  // long horizons, reproducible or debug builds
+  mpcqp_ws* other = nullptr;
+  {
+    std::lock_guard<std::mutex> lk(g_serve_mu);
+    other = g_server[ws->device & 63];
+    g_server[ws->device & 63] = ws;
+  }
+  if (other && other != ws) serve_stop(other);
   if (!ws->serve_box) {
     int cur = -1;
     hipError_t e = hipGetDevice(&cur);
@@ -477,6 +506,10 @@ int mpcqp_solve_served(mpcqp_ws* ws) {
     L.out = ws->stage_out_d;
     for (int i = 0; i < 6; ++i) L.off[i] = off[i];
     L.idle_ticks = 200000;  // 2 ms at 100 MHz
+    if (ws->serve_fault == 1) {  // mpcqp_debug_serve_fault: this launch is refused
+      ws->serve_fault = 0;
+      return fail(MPCQP_E_HIP, "k_serve launch: refused (mpcqp_debug_serve_fault)");
+    }
     launch(ws->stage_stream, ws->p, L);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return fail(MPCQP_E_HIP, std::string("k_serve launch: ") + hipGetErrorString(e));
@@ -510,6 +543,11 @@ int mpcqp_solve_served(mpcqp_ws* ws) {
         return fail(MPCQP_E_DEVICE, std::string("B=1 server: ") + hipGetErrorString(q));
       }
       if (std::chrono::steady_clock::now() - t_start > std::chrono::seconds(30)) {
+        // a stuck or queued wave may still write the output block: tell it to leave, and refuse every
+        // later request on this workspace rather than hand its blocks to a new one
+        __atomic_store_n(&box->req, mpcqp::kServeStop, __ATOMIC_RELEASE);
+        ws->serve_live = false;
+        ws->serve_broken = true;
         return fail(MPCQP_E_DEVICE, "B=1 server: no answer within 30 s");
       }
     }
@@ -527,6 +565,24 @@ int mpcqp_state_stride(int horizon) { return (int)ws_state_stride(horizon, horiz
 int mpcqp_ws_state_stride(const mpcqp_ws* ws) {
   if (!ws) return fail(MPCQP_E_ARG, "null ws");
   return (int)ws_state_stride(ws->p.horizon, mpcqp::wide_solve(ws->p));
+}
+
+int mpcqp_debug_serve_fault(mpcqp_ws* ws, int mode) {
+  if (!ws) return fail(MPCQP_E_ARG, "null ws");
+  if (mode == 1) {  // the next server launch is refused
+    ws->serve_fault = 1;
+    return MPCQP_OK;
+  }
+  if (mode == 2) {  // the live wave leaves now, behind the host's back (serve_live stays set)
+    if (!ws->serve_live) return fail(MPCQP_E_STATE, "no live server");
+    auto* box = static_cast<mpcqp::ServeBox*>(ws->serve_box);
+    __atomic_store_n(&box->req, mpcqp::kServeStop, __ATOMIC_RELEASE);
+    (void)hipStreamSynchronize(ws->stage_stream);
+    __atomic_store_n(&box->req, __atomic_load_n(&box->done, __ATOMIC_ACQUIRE), __ATOMIC_RELEASE);
+    return MPCQP_OK;
+  }
+  if (mode == 3) return ws->serve_live ? 1 : 0;  // query: a server is believed resident
+  return fail(MPCQP_E_ARG, "mode must be 1, 2 or 3");
 }
 
 int mpcqp_debug_stamps(unsigned long long* out32, int reset) {

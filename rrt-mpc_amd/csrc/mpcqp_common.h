@@ -516,6 +516,8 @@ struct mpcqp_ws {
   void* serve_box_d;
   uint32_t serve_seq;
   bool serve_live;
+  bool serve_broken;  // a request went unanswered (30 s): the workspace refuses B = 1 requests
+  int serve_fault;    // mpcqp_debug_serve_fault: 1 = refuse the next server launch
   std::chrono::steady_clock::time_point serve_last;  // the last completed request (host clock)
   // two QPs per wave for N <= 15 (MPCQP_PAIR_*, mpcqp_set_pairing)
   int pairing;

@@ -34,7 +34,7 @@ STATUS_NAMES = {
 
 # OSQP settings used by the reference (src/control/mpc_controller.py:121-131) plus the
 # OSQP defaults it relies on implicitly.
-ABI_VERSION = 8  # MPCQP_ABI_VERSION (include/mpcqp.h)
+ABI_VERSION = 9  # MPCQP_ABI_VERSION (include/mpcqp.h)
 # two QPs per wave for N <= 15 (mpcqp_set_pairing)
 PAIR_OFF, PAIR_ON, PAIR_AUTO = 0, 1, 2
 PAIRING_MODES = {"off": PAIR_OFF, "on": PAIR_ON, "auto": PAIR_AUTO}
@@ -270,6 +270,7 @@ _SYMBOLS = {
     "mpcqp_ws_state_stride": ([ctypes.c_void_p], ctypes.c_int),
     "mpcqp_debug_wave_ops": ([ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p], ctypes.c_int),
     "mpcqp_debug_stamps": ([ctypes.c_void_p, ctypes.c_int], ctypes.c_int),
+    "mpcqp_debug_serve_fault": ([ctypes.c_void_p, ctypes.c_int], ctypes.c_int),
     "mpcqp_stage": ([ctypes.c_void_p, ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_void_p),
                      ctypes.POINTER(ctypes.c_int32)], ctypes.c_int),
     "mpcqp_solve_staged": ([ctypes.c_void_p], ctypes.c_int),

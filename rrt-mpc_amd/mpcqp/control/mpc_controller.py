@@ -62,8 +62,19 @@ def _arr_key(a) -> bytes:
     return np.asarray(a, float).tobytes()
 
 
-def _tuple_key(a):
-    return a if type(a) is tuple else np.asarray(a, float).tobytes()
+_NUM = (float, int, np.floating, np.integer)
+
+
+def _tuple_key(a) -> tuple:
+    """Value key of a bounds field: a flat tuple of floats whatever the container (a tuple of tuples
+    of numbers takes the fast path; lists, arrays and tuples holding them are converted), so equal
+    bounds share one workspace and an unhashable leaf never reaches the cache."""
+    if type(a) is tuple:
+        if all(type(r) is tuple and all(isinstance(v, _NUM) for v in r) for r in a):
+            return tuple(float(v) for r in a for v in r)
+        if all(isinstance(v, _NUM) for v in a):
+            return tuple(float(v) for v in a)
+    return tuple(np.asarray(a, float).ravel().tolist())
 
 
 def _params_key(params, method: int, settings: dict) -> tuple:

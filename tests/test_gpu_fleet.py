@@ -36,13 +36,13 @@ def _branches(golden):
     return [br["spline"][off[i]:off[i + 1]] for i in range(len(off) - 1)]
 
 
-def _tracker(N, V, M, sim_steps, map_resolution=0.8, use_graph=True, fused=False):
+def _tracker(N, V, M, sim_steps, map_resolution=0.8, use_graph=True, fused=False, **settings):
     from mpcqp.config import MPCConfig
     from mpcqp.pipeline.fleet import FleetTracker
 
     mpc = MPCConfig(horizon=N, sim_steps=sim_steps)
     return FleetTracker(mpc, map_resolution=map_resolution, max_vehicles=V, max_ref_len=M, device="cuda:0",
-                        use_graph=use_graph, fused=fused)
+                        use_graph=use_graph, fused=fused, **settings)
 
 
 @pytest.mark.parametrize("fused", [False, True])

@@ -46,7 +46,7 @@ def test_library_exports_every_header_symbol():
         assert hasattr(handle, name), f"{name} declared in include/mpcqp.h but not exported"
     assert set(decls) == set(_lib_mod.exported_symbols())
     L = _lib_mod.lib()
-    assert L.mpcqp_version() == _lib_mod.ABI_VERSION == 8
+    assert L.mpcqp_version() == _lib_mod.ABI_VERSION == 9
     assert L.mpcqp_num_rows(20) == 101
     assert L.mpcqp_model_stride(20) % 8 == 0
 
@@ -420,3 +420,20 @@ def test_argument_checks_without_a_device():
     hin, hout = ctypes.c_void_p(), ctypes.c_void_p()
     offs = (ctypes.c_int32 * 6)()
     assert L.mpcqp_stage(None, ctypes.byref(hin), ctypes.byref(hout), offs) == E_ARG
+
+
+def test_params_key_normalises_bounds_containers():
+    """The B=1 controller cache keys bounds by value: tuples, lists, arrays and tuples of arrays of the
+    same numbers give one key (one workspace), and none of them is unhashable."""
+    import dataclasses
+
+    from mpcqp.config import MPCConfig
+    from mpcqp.control.mpc_controller import _params_key
+
+    p = MPCConfig(horizon=10).to_parameters(0.8)
+    forms = [p.du_bounds, [list(r) for r in p.du_bounds], np.asarray(p.du_bounds),
+             tuple(np.asarray(r) for r in p.du_bounds), tuple(tuple(np.float64(v) for v in r) for r in p.du_bounds)]
+    keys = {_params_key(dataclasses.replace(p, du_bounds=f), 0, {}) for f in forms}
+    assert len(keys) == 1
+    other = dataclasses.replace(p, du_bounds=((-1.0, 1.0), (-0.1, 0.1)))
+    assert _params_key(other, 0, {}) not in keys
