@@ -50,7 +50,7 @@ extern "C" {
 #define MPCQP_MAX_HORIZON 1024   /* per-QP workspace 16 (2N)^2 bytes: 67 MB at N = 1024 */
 #define MPCQP_WIDE_MIN_HORIZON 33 /* N <= 32: one wave per QP (2N <= 64 variables on the lanes, the KKT
                                      inverse in registers); N >= 33: one workgroup per QP */
-#define MPCQP_MID_MAX_HORIZON 63  /* 33 <= N <= 63 (fast mode): 2-4 x 1-2 waves per QP, the KKT inverse's
+#define MPCQP_MID_MAX_HORIZON 64  /* 33 <= N <= 64 (fast mode): 2-4 x 1-2 waves per QP, the KKT inverse's
                                      rows split in column parts over their registers; beyond, and in
                                      reproducible mode, 256 threads restating the C code */
 

@@ -15,6 +15,7 @@
 #include "mpcqp_build.h"
 
 #include <chrono>
+#include <cstdlib>
 #include <mutex>
 #ifdef MPCQP_ONLY_N
 #include "mpcqp_solve.h"  // development builds: one horizon, one translation unit
@@ -392,9 +393,12 @@ int mpcqp_stage(mpcqp_ws* ws, double** in, void** out, int32_t offsets[6]) {
     // the highest stream priority: the runtime gives each priority its own hardware queues, so the
     // resident server wave of mpcqp_solve_served never sits in a queue that torch's (default-priority)
     // streams share -- a queued packet behind a resident kernel waits until it leaves
+    // (MPCQP_SERVE_PRIORITY=default: the default priority instead -- diagnostics, tools/diag/serve_block.py)
     int least = 0, greatest = 0;
     if (e == hipSuccess) e = hipDeviceGetStreamPriorityRange(&least, &greatest);
-    if (e == hipSuccess) e = hipStreamCreateWithPriority(&st, hipStreamNonBlocking, greatest);
+    const char* pr = std::getenv("MPCQP_SERVE_PRIORITY");
+    const bool dflt = pr && std::strcmp(pr, "default") == 0;
+    if (e == hipSuccess) e = hipStreamCreateWithPriority(&st, hipStreamNonBlocking, dflt ? least : greatest);
     if (cur >= 0 && cur != ws->device) (void)hipSetDevice(cur);
     if (e != hipSuccess) {
       if (hin) (void)hipHostFree(hin);

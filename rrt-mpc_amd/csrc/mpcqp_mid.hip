@@ -1125,6 +1125,20 @@ __device__ __forceinline__ void mid_finish(const mpcqp_params& p, int b, Mid<NT>
     }
     if (activeo && k <= N)
       activeo[(size_t)b * (5 * N + 1) + k] = vk > p.v_bounds[1] ? 2 : (vk < p.v_bounds[0] ? 1 : 0);
+    // N = 64: the window has N + 1 = 65 states, one past the wave; state 64 is lane 63's inclusive sums
+    // (psi_64 = x02 + sum_{j < 64} si_j delta_j, X_64 = x0 + sum_{j < 64} t_j) with v_64 = W[126]
+    if (N + 1 > kWave && k == kWave - 1) {
+      const double p64 = x02 + sacc, v64 = sm.W[2 * (kWave - 1)];
+      if (Xo) {
+        double* Xb = Xo + (size_t)b * 4 * (N + 1);
+        Xb[0 * (N + 1) + kWave] = x00 + in0;
+        Xb[1 * (N + 1) + kWave] = x01 + in1;
+        Xb[2 * (N + 1) + kWave] = p64;
+        Xb[3 * (N + 1) + kWave] = v64;
+      }
+      if (activeo)
+        activeo[(size_t)b * (5 * N + 1) + kWave] = v64 > p.v_bounds[1] ? 2 : (v64 < p.v_bounds[0] ? 1 : 0);
+    }
     if (k == 0) {
       statuso[b] = status;
       if (iterso) {

@@ -78,13 +78,13 @@ _LOOP_BUFFERS = ("state", "u_prev", "path_idx", "phase", "steps", "trace", "u_tr
 
 
 @pytest.mark.parametrize("N,V,steps,seed,settings", [(15, 41, 80, 3, {}), (10, 64, 60, 11, {}),
-                                                      (15, 41, 80, 7, {"max_iter": 50, "polish_from": 0,
-                                                                        "polish_near": 0.0})])
+                                                      (15, 41, 80, 7, {"max_iter": 30, "polish": 0,
+                                                                        "polish_from": 0, "polish_near": 0.0})])
 def test_pair_fused_loop_equals_stepped_loop_bitwise(cuda, golden, N, V, steps, seed, settings):
     """The fused closed loop with two vehicles per wave (k_fleet_loop<N, true>: each half its own
     loop state and control flow; an odd fleet leaves the last wave one vehicle) == the graph-stepped
-    loop, every buffer bit for bit -- also with ADMM capped at 50 iterations, where unpolished
-    (solved_inaccurate) inputs drive the plant."""
+    loop, every buffer bit for bit -- also with the polish off and ADMM capped at 30 iterations, where
+    unpolished ADMM iterates drive the plant."""
     from test_gpu_fleet import _tracker, _varied_fleet
 
     g, paths, starts, goals = _varied_fleet(golden, V, seed=seed)
@@ -100,8 +100,8 @@ def test_pair_fused_loop_equals_stepped_loop_bitwise(cuda, golden, N, V, steps, 
     for k in _LOOP_BUFFERS:
         np.testing.assert_array_equal(bufs[0][k], bufs[1][k], err_msg=k)
     assert (res.phase != 0).any()
-    if settings:  # the capped case drives the plant with unpolished solves
-        assert (bufs[0]["status"] == 2).any()
+    if settings:  # unpolished solves drove the plant for many steps
+        assert (bufs[0]["steps"] > 20).any()
 
 
 def test_pair_fused_swarm_equals_stepped_swarm(cuda, golden):

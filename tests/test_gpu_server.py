@@ -80,11 +80,15 @@ def test_server_does_not_hold_default_priority_streams(cuda):
     from mpcqp.control.mpc_controller import BatchedMPCController
 
     b = scenarios.config3(8, horizon=10, seed=3)
+    streams = [torch.cuda.Stream() for _ in range(8)]
+    x = torch.zeros(8, device="cuda:0")
+    for i, s in enumerate(streams):  # the add kernel's first launch loads its code object: not measured here
+        with torch.cuda.stream(s):
+            x[i].add_(-1.0)
+    torch.cuda.synchronize()
     ctrl = BatchedMPCController(MPCConfig(horizon=10).to_parameters(0.8), 1, device="cuda:0")
     ctrl.solve_one(b.x0[0], b.ref[0], b.u_prev[0])
     assert _live(ctrl)
-    streams = [torch.cuda.Stream() for _ in range(8)]
-    x = torch.zeros(8, device="cuda:0")
     evs = []
     t0 = time.perf_counter()
     for i, s in enumerate(streams):
@@ -106,7 +110,7 @@ def test_server_does_not_hold_default_priority_streams(cuda):
     assert len(done) == 8, f"streams still blocked after 50 ms of served requests: {sorted(set(range(8)) - set(done))}"
     assert max(done.values()) < 0.01, done
     torch.cuda.synchronize()
-    assert torch.equal(x.cpu(), torch.ones(8))
+    assert torch.equal(x.cpu(), torch.zeros(8))
     ctrl.close()
 
 
@@ -169,7 +173,7 @@ def test_server_failure_paths(cuda, monkeypatch):
 
 
 @pytest.mark.parametrize("capped", [dict(max_iter=50, polish_from=0, polish_near=0.0),
-                                    dict(max_iter=60, polish=0, polish_from=0, polish_near=0.0)])
+                                    dict(max_iter=30, polish=0, polish_from=0, polish_near=0.0)])
 def test_served_unpolished_and_nan_against_launch(cuda, monkeypatch, capped):
     """Unpolished results (ADMM capped at max_iter, with and without the polish) and NaN inputs on
     the served path against a launch per call: statuses, the four counters and U equal bit for bit

@@ -96,7 +96,8 @@ def test_long_horizons_bit_exact_with_c_restatement(cuda, N, settings):
 
 
 @pytest.mark.parametrize("N,settings", [(32, {}), (33, {}), (40, {}), (41, {}),
-                                        (48, {"polish_from": 0, "polish_near": 0.0}), (52, {}), (56, {}), (63, {})])
+                                        (48, {"polish_from": 0, "polish_near": 0.0}), (52, {}), (56, {}), (63, {}),
+                                        (64, {})])
 def test_long_horizons_fast_mode_against_c_restatement(cuda, N, settings):
     """The default (fast) long-horizon mode (the mid kernel from N = 33, the one-wave kernel at N = 32): the
     same optimum, statuses, active sets
