@@ -611,7 +611,11 @@ def lib_key() -> str:
     the hash of the sources it was built from (mpcqp_build_id, __graft_entry__.source_hash)."""
     from mpcqp import _lib
 
-    return _lib.build_id()[:16]
+    if hasattr(_lib.lib(), "mpcqp_build_id"):
+        return _lib.build_id()[:16]
+    import hashlib  # a development library without a build id (tools/ab_lib.py)
+
+    return hashlib.sha256(Path(_lib.LIB_PATH).read_bytes()).hexdigest()[:16]
 
 
 def method_label(cparams) -> str:
@@ -995,7 +999,7 @@ def main() -> int:
                         args.pairing == "on" or (args.pairing == "auto" and
                                                  B > 8 * torch.cuda.get_device_properties(device).multi_processor_count)))},
                 "parallelism": f"dp{world} (independent contiguous shards, {'strong' if strong else 'weak'})",
-                "build_id": _lib.build_id(),
+                "build_id": _lib.build_id() if hasattr(L, "mpcqp_build_id") else None,
             },
             "solved_fraction": solved_all / total,
             "iters_mean": {"admm": admm_all / total, "polish": pol_all / total},

@@ -345,6 +345,16 @@ struct Unroll {
 // point (wavefront-scope fence), not an s_barrier with its lgkmcnt(0) drain.
 __device__ __forceinline__ void lds_sync() { __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront"); }
 
+// ------------------------------------------------------------------ phase marks
+// Built only with -DMPCQP_PHASE_MARKS for static analysis of the device assembly (never in the measured
+// library): an assembly comment where a solver phase begins, so tools/isa_breakdown.py can attribute
+// every instruction of k_solve<N> to the phase it executes in and weight it by the phase's count.
+#ifdef MPCQP_PHASE_MARKS
+#define MPCQP_MARK(name) asm volatile(";@phase " name)
+#else
+#define MPCQP_MARK(name)
+#endif
+
 // ------------------------------------------------------------------ diagnostic stamps
 // Built only with -DMPCQP_STAMPS (never in the measured library): per-phase s_memtime
 // cycle sums, flushed once per wave into g_stamps[] (read by mpcqp_debug_stamps).

@@ -45,8 +45,12 @@ struct SetupSmem {
   double buf[kWave];
   double model[kModelKept<N> ? 1 : model_stride(N)];
   double pre[4][N + 1];  // prefix sums of alpha, beta, gamma, eta
-  double err[N + 1][4];  // free-response tracking error e_m = sx_m - r_m
+  double err[4][N + 1];  // free-response tracking error e_m = sx_m - r_m, component-major
   double g[n];
+  // the input-cost band of H by row offset d = i - col in [-(n - 1), n - 1] (index d + n - 1), for the
+  // four kinds of column: speed, steering, the last speed (its a_k has no successor), none (zeros)
+  static constexpr int kBT = 2 * n - 1;
+  double bt[4][kBT];
 };
 
 template <int N>
@@ -463,6 +467,7 @@ __device__ __forceinline__ bool setup_qp(const mpcqp_params& p, int b, const dou
   Stamps T, T2;
   T2.begin();
   T.begin();
+  MPCQP_MARK("setup.k1");
 
   if constexpr (Win::kFleet) {  // the fleet loop: the vehicle's window -> LTV model into LDS
     double rx = 0.0, ry = 0.0, ryaw = 0.0, rv = 0.0;
@@ -498,28 +503,66 @@ __device__ __forceinline__ bool setup_qp(const mpcqp_params& p, int b, const dou
   const double* x0 = mdl + 11 * N + 4;
   const double* up = mdl + 11 * N + 8;
 
+  // the band table of the input cost (condensing below adds row i of its column's kind at offset
+  // i - lane): the same values the reference's R term puts on H's band
+  if constexpr (n < kWave) {
+    constexpr int kBT = SetupSmem<N>::kBT;
+    const double r00 = 0.5 * (p.r[0] + p.r[0]) / (dt * dt), r10 = 0.5 * (p.r[2] + p.r[1]) / dt;
+    const double r11 = 0.5 * (p.r[3] + p.r[3]);
+    for (int e = lane; e < 4 * kBT; e += LN::kLanes) {
+      const int kind = e / kBT, d = e % kBT - (n - 1);
+      double v = 0.0;
+      if (kind == 0 || kind == 2) {  // speed column (kind 2: the last one)
+        if (d == 0) v = kind == 0 ? 2.0 * r00 : r00;
+        if (d == 2 || d == -2) v = -r00;
+        if (d == 1) v = r10;
+        if (d == 3) v = -r10;
+      } else if (kind == 1) {  // steering column
+        if (d == 0) v = r11;
+        if (d == -1) v = r10;
+        if (d == -3) v = -r10;
+      }
+      (&sm.bt[0][0])[e] = v;
+    }
+  }
   // prefix sums (lanes 0..3, one array each) and free response (lane 4)
+  MPCQP_MARK("setup.prefix");
+  // ONE sequential recurrence on four lanes (one instruction stream): lanes 0 / 1 the prefix sums of
+  // alpha / gamma (pre[0] / pre[2]), lanes 2 / 3 the free response's x / y (W = 0: v_k = 0 for k >= 1,
+  // constant heading), acc <- acc + A[k] h + B[k] v_k + C[k] with (A, h, B, v, C) = (alpha | gamma, 1,
+  // -, 0, 0) on the prefix lanes -- exactly acc + A[k] (A * 1 and the zero terms are exact) -- and
+  // (alpha | gamma, psi, beta | eta, v_k, c0 | c1) on the free-response lanes, the reference's own
+  // expression.  The heading and speed rows of e_m are lane-parallel.
   if (lane < 4) {
-    const double* a = mdl + lane * N;
-    double acc = 0.0;
-    sm.pre[lane][0] = 0.0;
+    const bool fr = lane >= 2;
+    const int q = lane & 1;
+    // per-lane rows of the model block (immediate offsets k below); 1 / 0 multipliers select the terms
+    const double* __restrict__ A = mdl + (q ? 2 * N : 0);
+    const double* __restrict__ Bv = mdl + (q ? 3 * N : N);
+    const double* __restrict__ Cc = mdl + (q ? 6 * N : 5 * N);
+    const double* __restrict__ R = rr + 4 + q;
+    const double h = fr ? x0[2] : 1.0, v0 = fr ? x0[3] : 0.0, one = fr ? 1.0 : 0.0;
+    double acc = fr ? x0[q] : 0.0;
+    double* __restrict__ out = fr ? sm.err[q] : sm.pre[2 * q];
+    if (!fr) out[0] = 0.0;
+    // every load first (the model rows are not written here), then the dependent chain
+    double a[N], c[N], r[N];
+#pragma unroll
     for (int k = 0; k < N; ++k) {
-      acc += a[k];
-      sm.pre[lane][k + 1] = acc;
+      a[k] = A[k];
+      c[k] = Cc[k];
+      r[k] = R[4 * k];
     }
-  } else if (lane == 4) {  // free response at W = 0: v_k = 0 for k >= 1, constant heading
-    double px = x0[0], py = x0[1];
-    const double psi = x0[2];
-    for (int m = 1; m <= N; ++m) {
-      const int k = m - 1;
-      const double v = k == 0 ? x0[3] : 0.0;
-      px = px + al[k] * psi + be[k] * v + c0[k];
-      py = py + ga[k] * psi + et[k] * v + c1[k];
-      sm.err[m][0] = px - rr[4 * m + 0];
-      sm.err[m][1] = py - rr[4 * m + 1];
-      sm.err[m][2] = psi - rr[4 * m + 2];
-      sm.err[m][3] = 0.0 - rr[4 * m + 3];
+    const double b0 = Bv[0];
+#pragma unroll
+    for (int k = 0; k < N; ++k) {
+      acc = acc + a[k] * h + (k == 0 ? b0 : 0.0) * (k == 0 ? v0 : 0.0) + one * c[k];
+      out[k + 1] = acc - one * r[k];
     }
+  }
+  if (lane >= 1 && lane <= N) {
+    sm.err[2][lane] = x0[2] - rr[4 * lane + 2];
+    sm.err[3][lane] = 0.0 - rr[4 * lane + 3];
   }
   __syncthreads();
   T.end(0);
@@ -530,101 +573,122 @@ __device__ __forceinline__ bool setup_qp(const mpcqp_params& p, int b, const dou
   // The column stays in registers (Pc) through the scaling; static indices need the m loop
   // fully unrolled.
   // At n = 64 (N = 32) no lane is left over for g: the second branch.
+  MPCQP_MARK("setup.condense");
   double Pc[n];
   if constexpr (n < kWave) {
 #pragma unroll
     for (int i = 0; i < n; ++i) Pc[i] = 0.0;
     if (lane <= n) {
-      double Q[4][4], QN[4][4];
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          Q[i][j] = 0.5 * (p.q[4 * i + j] + p.q[4 * j + i]);
-          QN[i][j] = 0.5 * (p.q_terminal[4 * i + j] + p.q_terminal[4 * j + i]);
-        }
-      const int j = lane >> 1;
+      // Every lane runs the same instruction stream: the free-response column (lane n, which yields g)
+      // and the two kinds of decision-variable column differ only in lane constants and in which LDS
+      // row a lane reads per step, so the recursion has no branch and its loads pipeline.  Per step m
+      // the column's state sensitivity is s = (s0, s1, s2, s3):
+      //   speed v_{j+1} (cc = 0):      (be_{j+1}, et_{j+1}, 0, 0) from m = j + 2 on, (0, 0, 0, 1) at m = j + 1
+      //   steering delta_j (cc = 1):   si_j (P_a[m] - P_a[j+1], P_g[m] - P_g[j+1], 1, 0) from m = j + 1 on
+      //   free response (lane n):      e_m
+      // s0 = fma(k, X0[m] - o0, b0) (s1 alike), s2 = fma(kg, X2[m], c2), s3 = fma(kg, X3[m], c3), each
+      // gated to 0 before the column's first step: the values of the case analysis, exactly.
       const bool gcol = lane == n;
-      const double sj = gcol ? 0.0 : si[j];
+      const int j = lane >> 1;
+      const double sj = gcol ? 1.0 : si[j];
       const double pa0 = gcol ? 0.0 : sm.pre[0][j + 1], pg0 = gcol ? 0.0 : sm.pre[2][j + 1];
       const double bj = (!gcol && j + 1 < N) ? be[j + 1] : 0.0, ej = (!gcol && j + 1 < N) ? et[j + 1] : 0.0;
-      double mu0 = 0.0, mu1 = 0.0, mu2 = 0.0;
+      const bool st = gcol || cc == 1;  // s0 / s1 from the prefix sums (or e_m)
+      const double k01 = st ? sj : 0.0, o0 = st ? pa0 : 0.0, o1 = st ? pg0 : 0.0;
+      const double b0 = st ? 0.0 : bj, b1 = st ? 0.0 : ej;
+      const double kg = gcol ? 1.0 : 0.0;
+      const double c2v = (!gcol && cc == 1) ? sj : 0.0;
+      // thresholds: s0 / s1 live for m > t01, s2 for m > t2, s3 == 1 at m == t3
+      const int t01 = gcol ? 0 : (cc == 1 ? j : j + 1);
+      const int t2 = gcol ? 0 : j;
+      const int t3 = (!gcol && cc == 0) ? j + 1 : -1;
+      const double* X0 = gcol ? sm.err[0] : sm.pre[0];
+      const double* X1 = gcol ? sm.err[1] : sm.pre[2];
+      const double* X2 = gcol ? sm.err[2] : sm.pre[0];  // kg = 0: read, not used
+      const double* X3 = gcol ? sm.err[3] : sm.pre[0];
+      // the cost weights: Q / Q_N symmetrised, diagonal in the default parameters (a uniform branch)
+      bool diag = true;
 #pragma unroll
-      for (int m = N; m >= 1; --m) {
-        double s0, s1, s2, s3;
-        if (gcol) {
-          s0 = sm.err[m][0];
-          s1 = sm.err[m][1];
-          s2 = sm.err[m][2];
-          s3 = sm.err[m][3];
-        } else if (m > j) {
-          if (cc == 0) {  // v_{j+1}: itself at m = j+1, the positions from m = j+2 on
-            s0 = m >= j + 2 ? bj : 0.0;
-            s1 = m >= j + 2 ? ej : 0.0;
-            s2 = 0.0;
-            s3 = m == j + 1 ? 1.0 : 0.0;
-          } else {
-            s0 = sj * (sm.pre[0][m] - pa0);
-            s1 = sj * (sm.pre[2][m] - pg0);
-            s2 = sj;
-            s3 = 0.0;
+      for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int b = 0; b < 4; ++b)
+          if (a != b) diag = diag && p.q[4 * a + b] == 0.0 && p.q_terminal[4 * a + b] == 0.0;
+      double mu0 = 0.0, mu1 = 0.0, mu2 = 0.0;
+      auto recursion = [&](auto is_diag) {
+        constexpr bool kDiag = decltype(is_diag)::value;
+        if constexpr (kDiag)
+          MPCQP_MARK("setup.condense");
+        else
+          MPCQP_MARK("setup.condense_full_q");
+        double Q[4][4], QN[4][4];
+#pragma unroll
+        for (int a = 0; a < 4; ++a)
+#pragma unroll
+          for (int b = 0; b < 4; ++b) {
+            Q[a][b] = 0.5 * (p.q[4 * a + b] + p.q[4 * b + a]);
+            QN[a][b] = 0.5 * (p.q_terminal[4 * a + b] + p.q_terminal[4 * b + a]);
           }
-        } else {
-          s0 = s1 = s2 = s3 = 0.0;
-        }
-        const bool term = m == N;
-        auto W = [&](int i, int k) -> double { return term ? QN[i][k] : Q[i][k]; };
-        const double w0 = W(0, 0) * s0 + W(0, 1) * s1 + W(0, 2) * s2 + W(0, 3) * s3;
-        const double w1 = W(1, 0) * s0 + W(1, 1) * s1 + W(1, 2) * s2 + W(1, 3) * s3;
-        const double w2 = W(2, 0) * s0 + W(2, 1) * s1 + W(2, 2) * s2 + W(2, 3) * s3;
-        const double w3 = W(3, 0) * s0 + W(3, 1) * s1 + W(3, 2) * s2 + W(3, 3) * s3;
-        // row v_m: its own cost term + the positions after it; row delta_{m-1}: si * heading adjoint
-        double ha;
-        if (m < N) {
-          const double m0 = mu0, m1 = mu1;
-          ha = w3 + (be[m] * m0 + et[m] * m1);
-          mu0 = w0 + m0;
-          mu1 = w1 + m1;
-          mu2 = w2 + (mu2 + al[m] * m0 + ga[m] * m1);
-        } else {
-          ha = w3;
-          mu0 = w0;
-          mu1 = w1;
-          mu2 = w2;
-        }
-        const double hd = si[m - 1] * mu2;
-        if (gcol) {
-          sm.g[2 * (m - 1)] = ha;
-          sm.g[2 * (m - 1) + 1] = hd;
-        } else {
+#pragma unroll
+        for (int m = N; m >= 1; --m) {
+          double s0 = fma(k01, X0[m] - o0, b0);
+          double s1 = fma(k01, X1[m] - o1, b1);
+          s0 = m > t01 ? s0 : 0.0;
+          s1 = m > t01 ? s1 : 0.0;
+          const double s2 = fma(kg, X2[m], m > t2 ? c2v : 0.0);
+          const double s3 = fma(kg, X3[m], m == t3 ? 1.0 : 0.0);
+          const bool term = m == N;
+          auto W = [&](int i, int k) -> double { return term ? QN[i][k] : Q[i][k]; };
+          double w0, w1, w2, w3;
+          if constexpr (kDiag) {
+            w0 = W(0, 0) * s0;
+            w1 = W(1, 1) * s1;
+            w2 = W(2, 2) * s2;
+            w3 = W(3, 3) * s3;
+          } else {
+            w0 = W(0, 0) * s0 + W(0, 1) * s1 + W(0, 2) * s2 + W(0, 3) * s3;
+            w1 = W(1, 0) * s0 + W(1, 1) * s1 + W(1, 2) * s2 + W(1, 3) * s3;
+            w2 = W(2, 0) * s0 + W(2, 1) * s1 + W(2, 2) * s2 + W(2, 3) * s3;
+            w3 = W(3, 0) * s0 + W(3, 1) * s1 + W(3, 2) * s2 + W(3, 3) * s3;
+          }
+          // row v_m: its own cost term + the positions after it; row delta_{m-1}: si * heading adjoint
+          double ha;
+          if (m < N) {
+            const double m0 = mu0, m1 = mu1;
+            ha = w3 + (be[m] * m0 + et[m] * m1);
+            mu0 = w0 + m0;
+            mu1 = w1 + m1;
+            mu2 = w2 + (mu2 + al[m] * m0 + ga[m] * m1);
+          } else {
+            ha = w3;
+            mu0 = w0;
+            mu1 = w1;
+            mu2 = w2;
+          }
           Pc[2 * (m - 1)] = ha;
-          Pc[2 * (m - 1) + 1] = hd;
+          Pc[2 * (m - 1) + 1] = si[m - 1] * mu2;
         }
-      }
-      // input cost sum_k U_k' R U_k with a_k = (v_{k+1} - v_k)/dt: a band of column `lane`
-      const double r00 = 0.5 * (p.r[0] + p.r[0]) / (dt * dt), r10 = 0.5 * (p.r[2] + p.r[1]) / dt;
-      const double r11 = 0.5 * (p.r[3] + p.r[3]);
+      };
+      if (diag)
+        recursion(std::true_type{});
+      else
+        recursion(std::false_type{});
+      MPCQP_MARK("setup.gcol");
+      if (gcol)  // the free-response column is g
+#pragma unroll
+        for (int i = 0; i < n; ++i) sm.g[i] = Pc[i];
+      // input cost sum_k U_k' R U_k with a_k = (v_{k+1} - v_k)/dt: a band of column `lane`, read from
+      // the band table at offset i - lane (one LDS read per row at an immediate offset; a compare-and-
+      // select per row and band entry cost ~25 instructions a row)
+      MPCQP_MARK("setup.band");
       if (gcol) {  // the v_0 = x0[3] end of a_0
+        const double r00 = 0.5 * (p.r[0] + p.r[0]) / (dt * dt), r10 = 0.5 * (p.r[2] + p.r[1]) / dt;
         sm.g[0] += -x0[3] * r00;
         sm.g[1] += -x0[3] * r10;
-      } else {
-#pragma unroll
-        for (int i = 0; i < n; ++i) {
-          const int d = i - lane;
-          double add = 0.0;
-          if (cc == 0) {
-            if (d == 0) add = lane + 2 < n ? 2.0 * r00 : r00;
-            if (d == 2 || d == -2) add = -r00;
-            if (d == 1) add = r10;
-            if (d == 3) add = -r10;
-          } else {
-            if (d == 0) add = r11;
-            if (d == -1) add = r10;
-            if (d == -3) add = -r10;
-          }
-          Pc[i] += add;
-        }
       }
+      const int kind = gcol ? 3 : (cc == 1 ? 1 : (lane + 2 < n ? 0 : 2));
+      const double* tb = &sm.bt[kind][n - 1 - lane];
+#pragma unroll
+      for (int i = 0; i < n; ++i) Pc[i] += tb[i];
     }
     __syncthreads();
     if (!act)
@@ -661,10 +725,10 @@ __device__ __forceinline__ bool setup_qp(const mpcqp_params& p, int b, const dou
         constexpr int m = N - decltype(mc)::value;
         double s0, s1, s2, s3;
         if (gcol) {
-          s0 = sm.err[m][0];
-          s1 = sm.err[m][1];
-          s2 = sm.err[m][2];
-          s3 = sm.err[m][3];
+          s0 = sm.err[0][m];
+          s1 = sm.err[1][m];
+          s2 = sm.err[2][m];
+          s3 = sm.err[3][m];
         } else if (m > j) {
           if (cc == 0) {
             s0 = m >= j + 2 ? bj : 0.0;
@@ -740,6 +804,7 @@ __device__ __forceinline__ bool setup_qp(const mpcqp_params& p, int b, const dou
   T.begin();
 
   // ---- unscaled data: P = 2H (column `lane`), q = 2g, folded row bounds ----
+  MPCQP_MARK("setup.unscaled");
   double qv = act ? 2.0 * sm.g[lane] : 0.0;
   double cmx[4] = {0.0, 0.0, 0.0, 0.0};  // column max of |P| (partial maxima)
 #pragma unroll
@@ -788,6 +853,7 @@ __device__ __forceinline__ bool setup_qp(const mpcqp_params& p, int b, const dou
     return y * fma(-0.5 * v, y * y, 1.5);
   };
   double cpend = 1.0;  // cost factor not yet applied to Pc
+  MPCQP_MARK("setup.ruiz");
   for (int it = 0; it < p.scaling; ++it) {
     // column norms of [P; A] (first n columns of the KKT matrix): the lane's own rows and
     // the banded rows 2 and 4 ahead
@@ -840,6 +906,7 @@ __device__ __forceinline__ bool setup_qp(const mpcqp_params& p, int b, const dou
   //      moved from the column-per-lane setup layout to the row-major solve layout ----
   // symmetric Pbar = the lower triangle (row i >= column lane, computed by column `lane`)
   bool finite = isfinite(qv) && isfinite(cscale);
+  MPCQP_MARK("setup.write");
   lds_sync();  // setup's LDS data is dead: Pbar overwrites it
   if constexpr (kPackedP<N>) {
     double* Pb = lds.solve.P;
@@ -941,6 +1008,7 @@ __device__ __forceinline__ bool setup_qp(const mpcqp_params& p, int b, const dou
   }
   T.end(4);
   T2.end(0);
+  MPCQP_MARK("ctl");
   T.flush(16);   // g_stamps[16..20]: model/prefixes, condensing, unscaled data, Ruiz, Pbar + context
   T2.flush(21);  // g_stamps[21]: whole setup
   return bad_input;
@@ -972,6 +1040,7 @@ __device__ __forceinline__ int polish_qp(Ctx<N, Pair>& C, double& x, const doubl
   double rwf[3] = {0.0, 0.0, 0.0};  // soft-row weights of the current factorization
   bool have_fact = false;
   for (int pass = 0; pass < max_it; ++pass) {
+    MPCQP_MARK("pol.ctl");
     ++pol_it;
     C.opaque();
     double rw[3], tmp[3];
@@ -997,6 +1066,7 @@ __device__ __forceinline__ int polish_qp(Ctx<N, Pair>& C, double& x, const doubl
       for (int r = 0; r < 3; ++r) {
         uint64_t m = chg[r];
         while (m && !refac) {
+          MPCQP_MARK("pol.rank1");
           const int l = __builtin_ctzll(m);
           m &= m - 1;
           refac = !C.rank1(r, l, LN::readv(rw[r] - rwf[r], l));
@@ -1005,13 +1075,17 @@ __device__ __forceinline__ int polish_qp(Ctx<N, Pair>& C, double& x, const doubl
       }
       T.end(1);
     }
+    MPCQP_MARK("pol.ctl");
     if (refac) {
       T.begin();
+      MPCQP_MARK("pol.form");
       C.form(0.0, rw);
       T.end(0);
       T.begin();
+      MPCQP_MARK("pol.sweep");
       const bool okf = C.sweep();
       T.end(1);
+      MPCQP_MARK("pol.ctl");
       ++C.n_full;
       if (LN::any(!okf)) {
         result = -1;
@@ -1023,6 +1097,7 @@ __device__ __forceinline__ int polish_qp(Ctx<N, Pair>& C, double& x, const doubl
 #pragma unroll
     for (int r = 0; r < 3; ++r) rwf[r] = rw[r];
     T.begin();
+    MPCQP_MARK("pol.solve");
     const double rhs = C.CTmul(tmp) - C.qv;
     double xn = C.inv_mul(rhs);
     double zn[3];
@@ -1041,6 +1116,7 @@ __device__ __forceinline__ int polish_qp(Ctx<N, Pair>& C, double& x, const doubl
     if (!LN::any(diff)) {
       // the set reproduces itself: one step of iterative refinement (res = rhs - M xn), then
       // accept if it still does
+      MPCQP_MARK("pol.refine");
       double t3[3];
 #pragma unroll
       for (int r = 0; r < 3; ++r) t3[r] = rw[r] * zn[r];
@@ -1071,6 +1147,7 @@ __device__ __forceinline__ int polish_qp(Ctx<N, Pair>& C, double& x, const doubl
     // lands on the minimizer in [0, 1] after a few pieces (two independent reductions a step).
     // P xn from the Newton system (P xn + q = -C' rw (C xn - bound)): no product with P.
     T.begin();
+    MPCQP_MARK("pol.ls");
     double tb[3];
 #pragma unroll
     for (int r = 0; r < 3; ++r)
@@ -1084,6 +1161,7 @@ __device__ __forceinline__ int polish_qp(Ctx<N, Pair>& C, double& x, const doubl
     const double lin = LN::sum(act ? (Px + C.qv) * dx : 0.0);
     double t = 1.0;
     for (int ls = 0; ls < 40; ++ls) {
+      MPCQP_MARK("pol.lstrial");
       ++n_ls;
       double g1 = 0.0, g2 = 0.0;
 #pragma unroll
@@ -1110,6 +1188,7 @@ __device__ __forceinline__ int polish_qp(Ctx<N, Pair>& C, double& x, const doubl
       t = tn;
       if (!LN::any(moved)) break;
     }
+    MPCQP_MARK("pol.lsend");
     x = x + t * dx;
     Px = Px + t * Pd;
     C.Cmul(x, zc);
@@ -1117,6 +1196,7 @@ __device__ __forceinline__ int polish_qp(Ctx<N, Pair>& C, double& x, const doubl
     for (int r = 0; r < 3; ++r) cd[r] = zc[r] > C.hi[r] ? 2 : (zc[r] < C.lo[r] ? 1 : 0);
     T.end(3);
   }
+  MPCQP_MARK("ctl");
   T.flush(8);  // g_stamps[8..11]: polish form, sweep/rank-1, solve+check, line search
   return result;
 }
@@ -1155,12 +1235,21 @@ __device__ __forceinline__ int admm_run(const mpcqp_params& p, Ctx<N, Pair>& C, 
     if (S.need_fact) {
       const double rw[3] = {S.rho, S.rho, S.rho};
       T.begin();
+      MPCQP_MARK("admm.form");
+#ifdef MPCQP_DIAG_FACT_TWICE  // diagnostic builds only: the marginal cost of an ADMM factorization
+      C.form(sg, rw);
+      (void)C.sweep();
+#pragma unroll
+      for (int j = 0; j < 2 * N; ++j) asm volatile("" : "+v"(C.r[j]));  // the first inverse is computed
+#endif
       C.form(sg, rw);
       T.end(0);
       ++S.nfact;
       T.begin();
+      MPCQP_MARK("admm.sweep");
       const bool okf = C.sweep();
       T.end(1);
+      MPCQP_MARK("admm.fctl");
       if (LN::any(!okf)) {
         ev = kAdmmBad;
         break;
@@ -1180,7 +1269,11 @@ __device__ __forceinline__ int admm_run(const mpcqp_params& p, Ctx<N, Pair>& C, 
       rpb[r] = rho * pb[r];
     }
     const double ir = 1.0 / rho, oma = 1.0 - alpha;
+    // the next termination check's iteration (a multiple of check_termination): a compare per
+    // iteration instead of an integer modulo (a dozen scalar instructions)
+    int next_check = (S.it / p.check_termination + 1) * p.check_termination;
     while (!S.need_fact && S.it < p.max_iter) {
+      MPCQP_MARK("admm.iter");
       const int it = ++S.it;
       C.opaque();
       T.begin();
@@ -1202,7 +1295,9 @@ __device__ __forceinline__ int admm_run(const mpcqp_params& p, Ctx<N, Pair>& C, 
         S.y[r] = rpb[r] * d;
       }
       T.end(2);
-      if (it % p.check_termination == 0 || it == p.max_iter) {
+      if (it == next_check || it == p.max_iter) {
+        MPCQP_MARK("admm.check");
+        if (it == next_check) next_check += p.check_termination;
         T.begin();
         // Residual norms (OSQP: unscaled for termination, scaled for the rho update).  The
         // lane maxima are combined before the wave reductions (max distributes), which keeps
@@ -1290,6 +1385,7 @@ __device__ __forceinline__ int admm_run(const mpcqp_params& p, Ctx<N, Pair>& C, 
       }
     }
   }
+  MPCQP_MARK("ctl");
   T.flush(0);  // g_stamps[0..3]: form, sweep, ADMM iteration body, termination checks
   return ev;
 }
@@ -1330,6 +1426,7 @@ __device__ __forceinline__ int finish_qp(const mpcqp_params& p, int b, const dou
   const bool admm_ok = admm_flag == kAdmmConverged;
   Stamps T3;
   T3.begin();
+  MPCQP_MARK("outputs");
   if (LN::any(!isfinite(x))) bad = true;
   int status;
   if (bad) {
@@ -1605,6 +1702,9 @@ __global__ __launch_bounds__(kWave, kSolveWavesPerEU<N>) void k_solve(mpcqp_para
   Stamps TK;
   TK.begin();
   Ctx<N> C;
+#ifdef MPCQP_DIAG_SETUP_TWICE  // diagnostic builds only: the marginal cost of the setup (tools/ab.py)
+  (void)setup_qp<N>(p, b, model, in_x0, in_ref, in_up, BatchWin{}, C, sm, state + (size_t)b * state_stride(N), dbg);
+#endif
   bool bad = setup_qp<N>(p, b, model, in_x0, in_ref, in_up, BatchWin{}, C, sm, state + (size_t)b * state_stride(N), dbg);
   const bool use_admm = p.method == MPCQP_METHOD_ADMM;
   AdmmState S;
@@ -1674,6 +1774,10 @@ __global__ __launch_bounds__(kWave, kSolveWavesPerEU<N>) void k_solve(mpcqp_para
     S.rho_change = false;
   }
   double U;
+#ifdef MPCQP_DIAG_OUTPUT_TWICE  // diagnostic builds only: the marginal cost of the outputs
+  finish_qp<N>(p, b, model, in_x0, in_ref, in_up, BatchWin{}, sm.model, C, x, x_admm, flag, do_polish, pol_ok, bad, S.it,
+               S.nfact, pol_it, n_ls, u0o, Xo, Uo, statuso, iterso, activeo, U);
+#endif
   finish_qp<N>(p, b, model, in_x0, in_ref, in_up, BatchWin{}, sm.model, C, x, x_admm, flag, do_polish, pol_ok, bad, S.it,
                S.nfact, pol_it, n_ls, u0o, Xo, Uo, statuso, iterso, activeo, U);
   TK.end(0);
