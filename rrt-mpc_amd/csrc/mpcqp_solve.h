@@ -341,8 +341,11 @@ struct Ctx {
     // u = A^{-1} c: c has at most three entries, so u is three columns of the inverse -- by
     // symmetry the lane's own registers r[lu], r[lu-2], r[lu-4] (A^{-1}[i][j] = -r_i[j])
     double u = k0 * pick<0, n>(lu);
+    MPCQP_MARK("pol.rank1");
     if (lu >= 2) u += k1 * pick<0, n>(lu - 2);
+    MPCQP_MARK("pol.rank1");
     if (lu >= 4) u += k2 * pick<0, n>(lu - 4);
+    MPCQP_MARK("pol.rank1");
     u = act ? -u : 0.0;
     const double cu = (k0 * LN::readv(u, lu) + k1 * LN::readv(u, lu >= 2 ? lu - 2 : 0)) +
                       k2 * LN::readv(u, lu >= 4 ? lu - 4 : 0);
@@ -363,6 +366,7 @@ struct Ctx {
   template <int LO, int HI>
   __device__ __forceinline__ double pick(int j) const {
     if constexpr (HI - LO <= 2) {
+      MPCQP_MARK("pol.pick_leaf");
       double v = r[LO];
       if constexpr (HI - LO == 2) v = j == LO + 1 ? r[LO + 1] : v;
       asm volatile("" : "+v"(v));

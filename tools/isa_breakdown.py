@@ -71,8 +71,9 @@ def parse(path: str, kernel: str) -> dict:
     return out
 
 
-def weights(work: dict) -> dict:
-    """Executions per QP of each phase, from the kernel's mean work counters."""
+def weights(work: dict, N: int) -> dict:
+    """Executions per QP of each phase, from the kernel's mean work counters.  A rank-1 update reads
+    three columns of the inverse through pick<>'s tree of uniform branches."""
     w = work["work_means"]
     passes = w["polish_pass"]
     return {
@@ -84,7 +85,10 @@ def weights(work: dict) -> dict:
         "admm.form": w["admm_factorization"], "admm.sweep": w["admm_factorization"],
         "admm.fctl": w["admm_factorization"],
         "admm.iter": w["admm_it"], "admm.check": w["check"],
-        "pol.ctl": passes, "pol.rank1": w["rank1_update"],
+        # the rank-1 update is inlined once per soft-row slot (3 copies, one runs per update); each
+        # copy reads three inverse columns through pick<>'s uniform branch tree, one leaf of ceil(n/2)
+        "pol.ctl": passes, "pol.rank1": w["rank1_update"] / 3.0,
+        "pol.pick_leaf": w["rank1_update"] / (3.0 * ((2 * N + 1) // 2)),
         "pol.form": w["polish_full_factorization"], "pol.sweep": w["polish_full_factorization"],
         "pol.solve": passes, "pol.refine": w["polish_full_factorization"],
         "pol.ls": max(0.0, passes - w["polish_full_factorization"]), "pol.lstrial": w["ls_trial"],
@@ -102,7 +106,8 @@ def main() -> None:
     ap.add_argument("--pmc-key", default="N20_B4096")
     a = ap.parse_args()
     stat = parse(a.asm, a.kernel)
-    W = weights(json.load(open(a.work))[a.which])
+    N = int(re.search(r"ILi(\d+)E", a.kernel).group(1))
+    W = weights(json.load(open(a.work))[a.which], N)
     classes = ["f64", *VALU_NON_F64, "salu", "s_nop", "s_waitcnt", "lds", "vmem"]
     rows = {}
     tot = collections.Counter()
