@@ -910,6 +910,11 @@ __device__ __forceinline__ bool setup_qp(const mpcqp_params& p, int b, const dou
   //      moved from the column-per-lane setup layout to the row-major solve layout ----
   // symmetric Pbar = the lower triangle (row i >= column lane, computed by column `lane`)
   bool finite = isfinite(qv) && isfinite(cscale);
+  // the model block itself (LTV coefficients, window, x0, u_prev): a non-finite input flags the QP
+  // even where the diagonal-cost condensing multiplies no zero weight into it (a position error at
+  // N = 1 has no decision variable to reach)
+#pragma unroll 4
+  for (int i = lane; i < 11 * N + 10; i += LN::kLanes) finite = finite && isfinite(mdl[i]);
   MPCQP_MARK("setup.write");
   lds_sync();  // setup's LDS data is dead: Pbar overwrites it
   if constexpr (kPackedP<N>) {
