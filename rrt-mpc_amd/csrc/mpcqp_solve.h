@@ -35,9 +35,11 @@ struct SolveSmem<N, true> {
 // packed index of (i, j), i / j any order
 __device__ __forceinline__ int tri_idx(int i, int j) { return i >= j ? (i * (i + 1)) / 2 + j : (j * (j + 1)) / 2 + i; }
 
+// the whole-wave kernels' pivot-column buffers of the sweep (Ctx::sweep): 1 KB per wave
+constexpr int kColBytes = 2 * kWave * 8;
 template <int N>
 constexpr bool kModelKept =
-    8 * (int)sizeof(SolveSmem<N>) + 64 * model_stride(N) <= 163840;
+    8 * ((int)sizeof(SolveSmem<N>) + kColBytes) + 64 * model_stride(N) <= 163840;
 
 template <int N>
 struct SetupSmem {
@@ -53,13 +55,16 @@ struct SetupSmem {
   double bt[4][kBT];
 };
 
-template <int N>
+template <int N, bool Pair = false>
 struct SolveLds {
   union {
     SetupSmem<N> setup;
     SolveSmem<N> solve;  // setup_qp writes Pbar when its own LDS data is dead
   };
   double model[kModelKept<N> ? model_stride(N) : 1];  // the model block, live to the end (kModelKept)
+  // the sweep's pivot columns, double buffered (Ctx::sweep; the pair layout keeps register
+  // broadcasts and allocates none: its 16 QPs per CU need every KB of the LDS)
+  double col[Pair ? 1 : 2 * kWave];
   __device__ double* model_ptr() { return kModelKept<N> ? model : setup.model; }
 };
 
@@ -86,6 +91,7 @@ struct Ctx {
   double cscale;
   static constexpr int kPS = SolveSmem<N>::kPS;  // Pbar row stride
   double* __restrict__ P;  // Pbar (LDS, row-major n x n, row stride kPS)
+  double* __restrict__ colb;  // SolveLds::col: the sweep's pivot-column broadcast buffers
   const double* __restrict__ band;  // SolveSmem::band
   static constexpr int kNW = (n + 15) / 16;  // 16-lane rows holding the n variables
   // KKT inverse, row `lane`: A^{-1}[lane][j] = -r[j] (symmetric sweep operator)
@@ -291,26 +297,71 @@ struct Ctx {
   }
   // Symmetric sweep operator on the rows in r[]: afterwards A^{-1} = -r (row `lane`).
   // Step k: every lane needs its own A[i][k] (register r[k]) and the pivot row A[k][j] =
-  // A[j][k] (symmetry) -- the column r[k] of all lanes, register-broadcast by bcast() and read
-  // through DPP row_newbcast, so each update r[j] += coef * A[k][j] is one v_fmac_f64_dpp.
-  // The pivot row itself is the same FMA with coef = 1/d - 1 (A[k][j] <- A[k][j] / d), so the
-  // update is uniform over lanes.  The step loop is unrolled at compile time (static register
-  // indices and DPP lane immediates).  false on a non-positive pivot.
+  // A[j][k] (symmetry) -- the column r[k] of all lanes, read by each 16-lane row from the QP's LDS
+  // buffer (the lane's row copy w[c] lane l = A[16c + (l & 15)][k]) and consumed through DPP
+  // row_newbcast, so each update r[j] += coef * A[k][j] is one v_fmac_f64_dpp.  The pivot row itself
+  // is the same FMA with coef = 1/d - 1 (A[k][j] <- A[k][j] / d), so the update is uniform over
+  // lanes.  The step loop is unrolled at compile time (static register indices and DPP lane
+  // immediates).  false on a non-positive pivot.
+  // The column goes through LDS (one ds_write as soon as the previous step has updated it, kNW reads
+  // of the row's values and one uniform read of the pivot; double buffered, the QP's own buffer -- a
+  // half's in the pair layout) rather than permlane swaps and readlanes: fourteen VALU instructions
+  // per pivot move to the LDS pipe, with a whole step of FMAs to hide the round trip -- 503 -> 442
+  // cycles per pivot at two waves per SIMD, 352 -> 345 for a lone wave, the same bits
+  // (tools/micro/sweep_bench.hip, profiles/r05_sweep_bench.json).
   __device__ __forceinline__ bool sweep() {
+    if constexpr (Pair) return sweep_pair();
+    bool ok = true;
+    int ln = lane;
+    asm volatile("" : "+v"(ln));
+    const int rl = ln & 15;
+    lds_sync();
+    colb[ln] = r[0];
+    Unroll<0, n>::run([&](auto kc) {
+      constexpr int k = decltype(kc)::value;
+      const double* bk = colb + (k & 1) * kWave;
+      lds_sync();
+      double w[4];
+      Unroll<0, kNW>::run([&](auto cc) {
+        constexpr int c = decltype(cc)::value;
+        w[c] = bk[16 * c + rl];
+      });
+      // the pivot A[k][k]: a vector reciprocal (v_rcp_f64 + two Newton steps, within an ulp of
+      // 1/d), no IEEE division sequence on the step's critical path
+      const double d = bk[k];
+      // DPP reads of a VGPR need two wait states after its write; tie the pad to w
+      asm volatile("s_nop 1" : "+v"(w[0]));
+      ok = ok && (d > 0.0) && isfinite(d);
+      double inv = __builtin_amdgcn_rcp(d);
+      inv = fma(inv, fma(-d, inv, 1.0), inv);
+      inv = fma(inv, fma(-d, inv, 1.0), inv);
+      const bool piv = lane == k;
+      const double ck = r[k] * inv;
+      const double coef = piv ? inv - 1.0 : -ck;
+      // the next pivot column first, published for the next step
+      if constexpr (k + 1 < n) {
+        fmac_bc<(k + 1) % 16>(r[k + 1], w[(k + 1) / 16], coef);
+        colb[((k + 1) & 1) * kWave + ln] = r[k + 1];
+      }
+      Unroll<0, n>::run([&](auto jc) {
+        constexpr int j = decltype(jc)::value;
+        if constexpr (j != k && j != k + 1) fmac_bc<j % 16>(r[j], w[j / 16], coef);
+      });
+      r[k] = piv ? -inv : ck;
+    });
+    lds_sync();
+    return ok;
+  }
+  // The pair layout's sweep: a half's broadcast is one permlane16 swap per word and the pivot comes
+  // from its DPP row -- staging those through LDS measured 8 % slower there (43.8M -> 40.2M QP/s at
+  // N = 15, B = 16384, profiles/r05_i_ab.json), so the pair kernel keeps the register broadcasts.
+  __device__ __forceinline__ bool sweep_pair() {
     bool ok = true;
     Unroll<0, n>::run([&](auto kc) {
       constexpr int k = decltype(kc)::value;
-      // the pivot A[k][k] (lane k's r[k]): by readlane, so 1/d is computed while the column's
-      // broadcast is in flight; then a vector reciprocal (v_rcp_f64 + two Newton steps, within an
-      // ulp of 1/d): no IEEE division sequence on the step's critical path
-      double d, w[4];
-      if constexpr (Pair) {  // the half's lane k, from its broadcast row
-        vbcast(r[k], w);
-        d = LN::pin(row_bc<k % 16>(w[k / 16]));
-      } else {
-        d = readlane(r[k], k);
-        vbcast(r[k], w);
-      }
+      double w[4];
+      vbcast(r[k], w);
+      const double d = LN::pin(row_bc<k % 16>(w[k / 16]));
       ok = ok && (d > 0.0) && isfinite(d);
       double inv = __builtin_amdgcn_rcp(d);
       inv = fma(inv, fma(-d, inv, 1.0), inv);
@@ -347,13 +398,29 @@ struct Ctx {
     if (lu >= 4) u += k2 * pick<0, n>(lu - 4);
     MPCQP_MARK("pol.rank1");
     u = act ? -u : 0.0;
-    const double cu = (k0 * LN::readv(u, lu) + k1 * LN::readv(u, lu >= 2 ? lu - 2 : 0)) +
-                      k2 * LN::readv(u, lu >= 4 ? lu - 4 : 0);
+    // u through LDS (the sweep's buffer), as the sweep broadcasts its pivot columns: the three entries
+    // of c'u by uniform reads, the rows for the update by the lanes (the pair layout: lane reads and
+    // its one-stage register broadcast, as its sweep)
+    double w[4], cu;
+    if constexpr (Pair) {
+      cu = (k0 * LN::readv(u, lu) + k1 * LN::readv(u, lu >= 2 ? lu - 2 : 0)) + k2 * LN::readv(u, lu >= 4 ? lu - 4 : 0);
+    } else {
+      int ln = lane;
+      asm volatile("" : "+v"(ln));
+      lds_sync();
+      colb[ln] = u;
+      lds_sync();
+      cu = (k0 * colb[lu] + k1 * colb[lu >= 2 ? lu - 2 : 0]) + k2 * colb[lu >= 4 ? lu - 4 : 0];
+      Unroll<0, kNW>::run([&](auto cc) {
+        constexpr int c = decltype(cc)::value;
+        w[c] = colb[16 * c + (ln & 15)];
+      });
+      asm volatile("s_nop 1" : "+v"(w[0]));
+    }
     const double den = 1.0 + delta * cu;
     if (!(den > kRank1Min) || !isfinite(den)) return false;
     const double m = (delta / den) * u;
-    double w[4];
-    vbcast(u, w);
+    if constexpr (Pair) vbcast(u, w);
     Unroll<0, n>::run([&](auto jc) {
       constexpr int j = decltype(jc)::value;
       fmac_bc<j % 16>(r[j], w[j / 16], m);
@@ -457,7 +524,7 @@ template <int N, class Win, bool Pair = false>
 __device__ __forceinline__ bool setup_qp(const mpcqp_params& p, int b, const double* __restrict__ model,
                                          const double* __restrict__ in_x0, const double* __restrict__ in_ref,
                                          const double* __restrict__ in_up, const Win& win, Ctx<N, Pair>& C,
-                                         SolveLds<N>& lds, double* __restrict__ scratch, double* __restrict__ dbg) {
+                                         SolveLds<N, Pair>& lds, double* __restrict__ scratch, double* __restrict__ dbg) {
   using LN = Lanes<Pair>;
   constexpr int n = 2 * N;
   SetupSmem<N>& sm = lds.setup;
@@ -972,6 +1039,7 @@ __device__ __forceinline__ bool setup_qp(const mpcqp_params& p, int b, const dou
   // non-finite data (NaN/inf in x0, ref or u_prev) -> status MPCQP_NUMERICAL_ERROR
   const bool bad_input = LN::any(!finite);
   C.init(lane, dt, lds.solve);
+  C.colb = lds.col;
   C.qv = qv;
   C.D = D;
   C.cscale = cscale;
@@ -1586,7 +1654,7 @@ __device__ __forceinline__ int finish_qp(const mpcqp_params& p, int b, const dou
 template <int N, class Win, bool Pair = false>
 __device__ __forceinline__ int solve_one(const mpcqp_params& p, int b, const double* __restrict__ model,
                                          const double* __restrict__ in_x0, const double* __restrict__ in_ref,
-                                         const double* __restrict__ in_up, const Win& win, SolveLds<N>& sm,
+                                         const double* __restrict__ in_up, const Win& win, SolveLds<N, Pair>& sm,
                                          double* __restrict__ u0o, double* __restrict__ Xo, double* __restrict__ Uo,
                                          int32_t* __restrict__ statuso, int32_t* __restrict__ iterso,
                                          uint8_t* __restrict__ activeo, double& Ulane) {
@@ -1816,7 +1884,7 @@ __global__ __launch_bounds__(kWave, kSolveWavesPerEU<N>) void k_solve_pair(mpcqp
                                                       double* __restrict__ Uo, int32_t* __restrict__ statuso,
                                                       int32_t* __restrict__ iterso, uint8_t* __restrict__ activeo) {
   static_assert(2 * N <= 30, "two QPs per wave need n = 2N <= 30 (a padding lane or two per half)");
-  __shared__ SolveLds<N> sm[2];
+  __shared__ SolveLds<N, true> sm[2];
   const int h = threadIdx.x >> 5;
   const int b = 2 * blockIdx.x + h;
   if (b >= B || (mask && !mask[b])) return;  // that half only: the other QP runs on
@@ -1842,10 +1910,10 @@ __global__ __launch_bounds__(kWave, kSolveWavesPerEU<N>) void k_fleet_loop(const
                                                                          mpcqp_fleet f, int steps,
                                                                          mpcqp::LoopTrigger tr) {
   using LN = Lanes<Pair>;
-  __shared__ SolveLds<N> smv[Pair ? 2 : 1];
+  __shared__ SolveLds<N, Pair> smv[Pair ? 2 : 1];
   __shared__ double lsv[Pair ? 12 : 6];  // loop state: x[4], u_prev[2] (per half)
   const int h = Pair ? (int)(threadIdx.x >> 5) : 0;
-  SolveLds<N>& sm = smv[h];
+  SolveLds<N, Pair>& sm = smv[h];
   double* const ls = lsv + 6 * h;
   const int slot = 2 * (int)blockIdx.x + h;  // pair: may be V (odd V)
   const int b = Pair ? ((tr.order && slot < f.vehicles) ? tr.order[slot] : slot)

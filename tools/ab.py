@@ -24,6 +24,8 @@ LEGS = {
     # lone waves: one QP per CU (256) and a single QP (the kernel event time is the QP's latency)
     "c3_b256": ["--batch", "256", "--check-sample", "64"],
     "c3_b1": ["--batch", "1", "--check-sample", "1"],
+    # two QPs per wave (N = 15)
+    "pair15": ["--horizon", "15", "--batch", "16384", "--pairing", "on", "--check-sample", "128"],
 }
 
 
