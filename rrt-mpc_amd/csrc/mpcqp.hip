@@ -589,6 +589,15 @@ int mpcqp_debug_serve_fault(mpcqp_ws* ws, int mode) {
   return fail(MPCQP_E_ARG, "mode must be 1, 2 or 3");
 }
 
+#ifdef MPCQP_STAMPS
+typedef hipError_t (*StampsFn)(unsigned long long* out32, int reset);
+static StampsFn g_stamp_parts[64];
+static int g_n_stamp_parts = 0;
+extern "C" void mpcqp_register_stamps(StampsFn f) {
+  if (g_n_stamp_parts < 64) g_stamp_parts[g_n_stamp_parts++] = f;
+}
+#endif
+
 int mpcqp_debug_stamps(unsigned long long* out32, int reset) {
 #ifdef MPCQP_STAMPS
   hipError_t e = hipDeviceSynchronize();
@@ -597,6 +606,7 @@ int mpcqp_debug_stamps(unsigned long long* out32, int reset) {
     unsigned long long z[32] = {0};
     e = hipMemcpyToSymbol(HIP_SYMBOL(g_stamps), z, sizeof(z));
   }
+  for (int i = 0; i < g_n_stamp_parts && e == hipSuccess; ++i) e = g_stamp_parts[i](out32, reset);
   if (e != hipSuccess) return fail(MPCQP_E_HIP, std::string("stamps: ") + hipGetErrorString(e));
   return MPCQP_OK;
 #else

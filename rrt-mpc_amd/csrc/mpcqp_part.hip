@@ -6,6 +6,28 @@
 #error "define MPCQP_PART_LO and MPCQP_PART_HI"
 #endif
 
+#ifdef MPCQP_STAMPS
+// diagnostic builds: this object's own g_stamps (every translation unit has its copy) joins the
+// registry mpcqp_debug_stamps sums over
+extern "C" void mpcqp_register_stamps(hipError_t (*f)(unsigned long long*, int));
+namespace {
+hipError_t part_stamps(unsigned long long* out32, int reset) {
+  hipError_t e = hipSuccess;
+  if (out32) {
+    unsigned long long v[32];
+    e = hipMemcpyFromSymbol(v, HIP_SYMBOL(g_stamps), sizeof(v));
+    for (int i = 0; i < 32 && e == hipSuccess; ++i) out32[i] += v[i];
+  }
+  if (e == hipSuccess && reset) {
+    unsigned long long z[32] = {0};
+    e = hipMemcpyToSymbol(HIP_SYMBOL(g_stamps), z, sizeof(z));
+  }
+  return e;
+}
+const int kRegistered = (mpcqp_register_stamps(part_stamps), 0);
+}  // namespace
+#endif
+
 namespace mpcqp {
 #if MPCQP_PART_LO <= 1 && 1 <= MPCQP_PART_HI
 template void launch_solve<1>(hipStream_t, const Launch&);

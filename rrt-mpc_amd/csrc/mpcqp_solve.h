@@ -309,8 +309,13 @@ struct Ctx {
   // per pivot move to the LDS pipe, with a whole step of FMAs to hide the round trip -- 503 -> 442
   // cycles per pivot at two waves per SIMD, 352 -> 345 for a lone wave, the same bits
   // (tools/micro/sweep_bench.hip, profiles/r05_sweep_bench.json).
+  // At n <= 32 (kNW <= 2) the register broadcast is a single permlane16 stage (none at n <= 16), and
+  // a lone wave (B = 1, the closed loops) would wait out the LDS round trip on every pivot: 5.6k
+  // against ~3.6k cycles per N = 10 factorization (profiles/r05_n_stamps/, r05_o_ab_register_sweep_n_le_32.json).  Those sizes
+  // and the pair layout keep the register broadcasts (sweep_reg).
+  static constexpr bool kRegBcast = Pair || kNW <= 2;
   __device__ __forceinline__ bool sweep() {
-    if constexpr (Pair) return sweep_pair();
+    if constexpr (kRegBcast) return sweep_reg();
     bool ok = true;
     int ln = lane;
     asm volatile("" : "+v"(ln));
@@ -352,16 +357,22 @@ struct Ctx {
     lds_sync();
     return ok;
   }
-  // The pair layout's sweep: a half's broadcast is one permlane16 swap per word and the pivot comes
-  // from its DPP row -- staging those through LDS measured 8 % slower there (43.8M -> 40.2M QP/s at
-  // N = 15, B = 16384, profiles/r05_i_ab.json), so the pair kernel keeps the register broadcasts.
-  __device__ __forceinline__ bool sweep_pair() {
+  // The register-broadcast sweep (n <= 32 and the pair layout): the column by vbcast, the pivot by
+  // readlane (whole wave; 1/d is computed while the broadcast is in flight) or from the half's DPP
+  // row (pair layout).  Staging through LDS measured 8 % slower in the pair layout (43.8M -> 40.2M
+  // QP/s at N = 15, B = 16384, profiles/r05_i_ab.json).
+  __device__ __forceinline__ bool sweep_reg() {
     bool ok = true;
     Unroll<0, n>::run([&](auto kc) {
       constexpr int k = decltype(kc)::value;
-      double w[4];
-      vbcast(r[k], w);
-      const double d = LN::pin(row_bc<k % 16>(w[k / 16]));
+      double d, w[4];
+      if constexpr (Pair) {
+        vbcast(r[k], w);
+        d = LN::pin(row_bc<k % 16>(w[k / 16]));
+      } else {
+        d = readlane(r[k], k);
+        vbcast(r[k], w);
+      }
       ok = ok && (d > 0.0) && isfinite(d);
       double inv = __builtin_amdgcn_rcp(d);
       inv = fma(inv, fma(-d, inv, 1.0), inv);
@@ -402,7 +413,7 @@ struct Ctx {
     // of c'u by uniform reads, the rows for the update by the lanes (the pair layout: lane reads and
     // its one-stage register broadcast, as its sweep)
     double w[4], cu;
-    if constexpr (Pair) {
+    if constexpr (kRegBcast) {
       cu = (k0 * LN::readv(u, lu) + k1 * LN::readv(u, lu >= 2 ? lu - 2 : 0)) + k2 * LN::readv(u, lu >= 4 ? lu - 4 : 0);
     } else {
       int ln = lane;
@@ -420,7 +431,7 @@ struct Ctx {
     const double den = 1.0 + delta * cu;
     if (!(den > kRank1Min) || !isfinite(den)) return false;
     const double m = (delta / den) * u;
-    if constexpr (Pair) vbcast(u, w);
+    if constexpr (kRegBcast) vbcast(u, w);
     Unroll<0, n>::run([&](auto jc) {
       constexpr int j = decltype(jc)::value;
       fmac_bc<j % 16>(r[j], w[j / 16], m);

@@ -26,6 +26,15 @@ LEGS = {
     "c3_b1": ["--batch", "1", "--check-sample", "1"],
     # two QPs per wave (N = 15)
     "pair15": ["--horizon", "15", "--batch", "16384", "--pairing", "on", "--check-sample", "128"],
+    "n10_b1": ["--horizon", "10", "--batch", "1", "--polish-from", "25", "--check-sample", "1"],
+    "n15_b1024": ["--horizon", "15", "--batch", "1024", "--pairing", "off", "--check-sample", "64"],
+    "n10_b1024": ["--horizon", "10", "--batch", "1024", "--pairing", "off", "--check-sample", "64"],
+    # a fixed schedule (150 ADMM iterations, no termination check, no polish): per-iteration costs
+    # of variants whose iterates differ
+    "c3_fixed": ["--set", "max_iter=150", "--set", "polish=0", "--set", "check_termination=1000",
+                 "--set", "adaptive_rho=0", "--check-sample", "0"],
+    "c3_b1_fixed": ["--batch", "1", "--set", "max_iter=150", "--set", "polish=0", "--set",
+                    "check_termination=1000", "--set", "adaptive_rho=0", "--check-sample", "0"],
 }
 
 
@@ -53,9 +62,11 @@ def main() -> None:
         for lib in a.libs:
             for leg in a.legs:
                 d = run(lib, LEGS[leg])
+                re_ = d.get("rel_err") or {"max_rel_err_U": 0.0, "active_set_mismatches": 0, "status_mismatches": 0}
                 rec = {"value": d["value"], "k_solve_ms": d["kernel_ms"]["k_solve"], "ms_per_step": d["ms_per_step"],
-                       "rel_err": d["rel_err"]["max_rel_err_U"], "iters_agreement": d["rel_err"].get("iters_agreement"),
-                       "mism": d["rel_err"]["active_set_mismatches"] + d["rel_err"]["status_mismatches"]}
+                       "rel_err": re_["max_rel_err_U"], "iters_agreement": re_.get("iters_agreement"),
+                       "mism": re_["active_set_mismatches"] + re_["status_mismatches"],
+                       "admm_iters": d["iters_mean"]["admm"], "polish_iters": d["iters_mean"]["polish"]}
                 res.setdefault(lib, {}).setdefault(leg, []).append(rec)
                 print(lib, leg, r, json.dumps(rec), flush=True)
             if a.b1:
@@ -74,7 +85,7 @@ def main() -> None:
             if leg == "b1":
                 summary[lib][leg] = {k: sum(x[k] for x in recs) / len(recs) for k in recs[0] if isinstance(recs[0][k], (int, float))}
             else:
-                summary[lib][leg] = {k: sum(x[k] for x in recs) / len(recs) for k in ("value", "k_solve_ms", "ms_per_step")}
+                summary[lib][leg] = {k: sum(x[k] for x in recs) / len(recs) for k in ("value", "k_solve_ms", "ms_per_step", "admm_iters", "polish_iters")}
                 summary[lib][leg]["worst_rel_err"] = max(x["rel_err"] for x in recs)
                 summary[lib][leg]["mismatches"] = sum(x["mism"] for x in recs)
                 summary[lib][leg]["iters_agreement_min"] = min((x["iters_agreement"] or 0) for x in recs)

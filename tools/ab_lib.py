@@ -26,6 +26,8 @@ def main() -> None:
     ap.add_argument("name")
     ap.add_argument("--parts", type=int, nargs="*", default=[], help="horizons whose part objects to recompile")
     ap.add_argument("--define", action="append", default=[], help="extra -D for the recompiled objects")
+    ap.add_argument("--sources", nargs="*", default=[],
+                    help="also recompile the objects of these source files (e.g. mpcqp.hip for a stamps build)")
     a = ap.parse_args()
     hipcc = "/opt/rocm/bin/hipcc"
     cmds = g._compile_jobs(hipcc)
@@ -36,7 +38,8 @@ def main() -> None:
         obj = c[c.index("-o") + 1]
         lo = next((int(x.split("=")[1]) for x in c if x.startswith("-DMPCQP_PART_LO=")), None)
         hi = next((int(x.split("=")[1]) for x in c if x.startswith("-DMPCQP_PART_HI=")), None)
-        if lo is not None and any(lo <= n <= hi for n in a.parts):
+        src = any(x.endswith(tuple("/" + f for f in a.sources)) for x in c) if a.sources else False
+        if src or (lo is not None and any(lo <= n <= hi for n in a.parts)):
             new = odir / Path(obj).name
             c2 = list(c)
             c2[c2.index("-o") + 1] = str(new)
