@@ -1816,7 +1816,11 @@ __global__ __launch_bounds__(kWave, kSolveWavesPerEU<N>) void k_solve(mpcqp_para
     int kind = 0;
     double zg[3];
     if (use_admm) {
+      Stamps TA;
+      TA.begin();
       const int ev = admm_run<N>(p, C, S);
+      TA.end(0);
+      TA.flush(4);  // g_stamps[4]: every admm_run call (slots 5..9 get zeros)
       if (ev == kAdmmAttempt) {
         kind = 1;
       } else {
