@@ -1255,8 +1255,10 @@ __device__ __forceinline__ int polish_qp(Ctx<N, Pair>& C, double& x, const doubl
       double g1 = 0.0, g2 = 0.0;
 #pragma unroll
       for (int r = 0; r < 3; ++r) {
+        // zt - clamp(zt, lo, hi): zt - hi above, zt - lo below, exactly 0 inside (the same values
+        // as the compare-and-select form, without its branches: zc, zd are finite here)
         const double zt = zc[r] + t * zd[r];
-        const double rr = zt > C.hi[r] ? zt - C.hi[r] : (zt < C.lo[r] ? zt - C.lo[r] : 0.0);
+        const double rr = zt - min_nc(max_nc(zt, C.lo[r]), C.hi[r]);
         g1 += 2.0 * C.wb[r] * rr * zd[r];
         if (rr != 0.0) g2 += 2.0 * C.wb[r] * zd[r] * zd[r];
       }
@@ -1269,10 +1271,9 @@ __device__ __forceinline__ int polish_qp(Ctx<N, Pair>& C, double& x, const doubl
       bool moved = false;
 #pragma unroll
       for (int r = 0; r < 3; ++r) {
+        // the piece (above / inside / below) changed: lo <= hi, so the two compares decide it
         const double za = zc[r] + t * zd[r], zb = zc[r] + tn * zd[r];
-        const int ca = za > C.hi[r] ? 2 : (za < C.lo[r] ? 1 : 0);
-        const int cb = zb > C.hi[r] ? 2 : (zb < C.lo[r] ? 1 : 0);
-        moved = moved || ca != cb;
+        moved = moved || ((za > C.hi[r]) != (zb > C.hi[r])) || ((za < C.lo[r]) != (zb < C.lo[r]));
       }
       t = tn;
       if (!LN::any(moved)) break;
