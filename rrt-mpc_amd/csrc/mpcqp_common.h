@@ -248,6 +248,7 @@ struct Lanes<false> {
   __device__ __forceinline__ static double shr4(double v) { return ::shr4(v); }
   __device__ __forceinline__ static double shl4(double v) { return ::shl4(v); }
   __device__ __forceinline__ static double shr1(double v) { return dpp<kWaveShr1>(v); }  // lane 0 <- 0
+  __device__ __forceinline__ static double shl1(double v) { return dpp<kWaveShl1>(v); }  // lane 63 <- 0
   __device__ __forceinline__ static double scan(double v, int lane) { return scan_add(v, lane); }
   __device__ __forceinline__ static double shfl(double v, int src) { return __shfl(v, src, kWave); }
 };
@@ -324,6 +325,10 @@ struct Lanes<true> {
   __device__ __forceinline__ static double shr1(double v) {
     const double d = pin(dpp<kWaveShr1>(v));
     return hl() >= 1 ? d : 0.0;
+  }
+  __device__ __forceinline__ static double shl1(double v) {
+    const double d = pin(dpp<kWaveShl1>(v));
+    return hl() < 31 ? d : 0.0;
   }
   __device__ __forceinline__ static double shfl(double v, int src) { return pin(__shfl(v, src, 32)); }
 };

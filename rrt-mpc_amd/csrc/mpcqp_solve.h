@@ -23,17 +23,24 @@ struct SolveSmem {
   double pad0[4];     // zeros: form()'s band writes of the first rows land here when out of range
   double P[n * kPS];  // Pbar, row-major (lane `col` reads column col: conflict-free; lanes >= n read the zeros of column n)
   double pad1[4];     // zeros: ... and those of the last rows
-  double band[5][n];  // Pbar's entries at form()'s band addresses (lane p: (p, p + 2d - 4)), restored after each form
+  double band[5][n];  // Pbar's entries at form()'s band addresses (lane p: (p, p + d - 2)), restored after each form
 };
 template <int N>
 struct SolveSmem<N, true> {
   static constexpr int n = 2 * N;
   static constexpr int kPS = 0;  // unused
   double P[kWave * (kWave + 1) / 2];  // lower triangle, packed by rows; rows >= n zero
-  double band[3][n];                  // Pbar's entries (p, p - 4), (p, p - 2), (p, p) (form() adds there)
+  double band[3][n];                  // Pbar's entries (p, p - 2), (p, p - 1), (p, p) (form() adds there)
 };
 // packed index of (i, j), i / j any order
 __device__ __forceinline__ int tri_idx(int i, int j) { return i >= j ? (i * (i + 1)) / 2 + j : (j * (j + 1)) / 2 + i; }
+// a variable lane's position in the reference-facing order W = (v_1, delta_0, v_2, delta_1, ...) (the
+// solver keeps the speeds in lanes 0..N-1 and the steering angles in lanes N..2N-1; Ctx); lanes past
+// the variables map to themselves
+template <int N>
+__device__ __forceinline__ int interleaved(int p) {
+  return p < N ? 2 * p : (p < 2 * N ? 2 * (p - N) + 1 : p);
+}
 
 // the whole-wave kernels' pivot-column buffers of the sweep (Ctx::sweep): 1 KB per wave
 constexpr int kColBytes = 2 * kWave * 8;
@@ -70,14 +77,18 @@ struct SolveLds {
 
 // ------------------------------------------------------------------ shared solver context
 // Per-lane view of one scaled QP plus the structured operators and the KKT inverse.
-// Variables W = (v_1, delta_0, v_2, delta_1, ...): lane 2j holds the speed v_{j+1}, lane 2j+1
-// the steering delta_j.  The rows owned by lane p (slot 0: v row, p even; slot 1: input row;
-// slot 2: rate row) are banded in those variables:
-//   slot 0  c0 x_p                                      (v_{p/2+1}: identity)
-//   slot 1  c10 x_p + c11 x_{p-2}                       (a_j = (v_{j+1} - v_j)/dt; delta_j)
-//   slot 2  c20 x_p + c21 x_{p-2} + c22 x_{p-4}         (a_j - a_{j-1}; delta_j - delta_{j-1})
+// Variables W = (v_1, ..., v_N, delta_0, ..., delta_{N-1}) in two blocks: lane j < N holds the speed
+// v_{j+1}, lane N + j the steering delta_j (interleaved<N>() gives a lane's position in the
+// reference-facing order v_1, delta_0, v_2, delta_1, ...).  The rows owned by lane p (slot 0: v row,
+// speed lanes; slot 1: input row; slot 2: rate row) are banded in those variables:
+//   slot 0  c0 x_p                                      (v_{p+1}: identity)
+//   slot 1  c10 x_p + c11 x_{p-1}                       (a_j = (v_{j+1} - v_j)/dt; delta_j)
+//   slot 2  c20 x_p + c21 x_{p-1} + c22 x_{p-2}         (a_j - a_{j-1}; delta_j - delta_{j-1})
 // with c = (row scaling E x row coefficient) x the column scaling D of the variable it multiplies:
-// the scaled operator Cbar = E C D with D folded into the coefficients.
+// the scaled operator Cbar = E C D with D folded into the coefficients.  "The same input one step
+// back" is one lane back, so the banded operators move values by one and two lanes (a 64-bit DPP
+// move per lane step); the coefficients that would reach across the block boundary (c11, c21, c22
+// of a block's first lanes) are exact zeros, so what a shift carries across it is multiplied away.
 template <int N, bool Pair = false>
 struct Ctx {
   using LN = Lanes<Pair>;
@@ -107,7 +118,7 @@ struct Ctx {
     n_full = 0;
     n_r1 = 0;
     act = ln < n;
-    even = act && ((ln & 1) == 0);
+    even = ln < N;  // the speed block
     dt = dt_;
     P = s.P;
   }
@@ -133,18 +144,18 @@ struct Ctx {
 
   // z = Cbar x: shifts only (no scans)
   __device__ __forceinline__ void Cmul(double x, double z[3]) const {
-    const double xm2 = LN::shr2(x);
-    const double xm4 = LN::shr2(xm2);
+    const double xm1 = LN::shr1(x);
+    const double xm2 = LN::shr1(xm1);
     z[0] = c0 * x;
-    z[1] = c10 * x + c11 * xm2;
-    z[2] = (c20 * x + c21 * xm2) + c22 * xm4;
+    z[1] = c10 * x + c11 * xm1;
+    z[2] = (c20 * x + c21 * xm1) + c22 * xm2;
   }
-  // x = Cbar' y: the terms for the variables 2 and 4 back shifted in one chain, shl2(a + shl2(b))
+  // x = Cbar' y: the terms for the variables 1 and 2 back shifted in one chain, shl1(a + shl1(b))
   __device__ __forceinline__ double CTmul(const double y[3]) const {
-    const double a = c11 * y[1] + c21 * y[2];  // to the variable 2 back
-    const double b = c22 * y[2];               // to the variable 4 back
+    const double a = c11 * y[1] + c21 * y[2];  // to the variable 1 back
+    const double b = c22 * y[2];               // to the variable 2 back
     const double t = (c0 * y[0] + c10 * y[1]) + c20 * y[2];
-    return t + LN::shl2(a + LN::shl2(b));
+    return t + LN::shl1(a + LN::shl1(b));
   }
   // (Pbar v)_lane, Pbar symmetric: lane reads its row as a conflict-free column of the LDS copy
   // The column loads go out in groups of kPG ahead of their FMAs (the inline-asm FMAs pin each
@@ -195,7 +206,7 @@ struct Ctx {
     return act ? (a[0] + a[1]) + (a[2] + a[3]) : 0.0;
   }
   // KKT matrix A = Pbar + s I + Cbar' diag(rw) Cbar, row `lane` -> r[].  The row part is a
-  // band (lanes p-4 .. p+4 of the same kind): its five entries per lane come from shifts.
+  // band (lanes p-2 .. p+2 of the same block): its five entries per lane come from shifts.
   // From n >= 8 on, each lane adds its five band entries into its own row of Pbar in LDS
   // (read-modify-write), every lane loads its row as a column of the sum, and the lanes write the
   // original entries back: ~10 VALU instructions instead of a compare-and-select per column (the
@@ -207,25 +218,25 @@ struct Ctx {
     // opaque lane copy: keeps per-column masks/addresses from being hoisted out of solver loops
     int ln = lane;
     asm volatile("" : "+v"(ln));
-    // row r of lane q (weight rw) adds rw c_i c_j at (q - 2i, q - 2j): lane p's diagonal takes its
-    // own rows' c_0 terms, lane p+2's c_1 terms and lane p+4's c_2 terms, and so on
+    // row r of lane q (weight rw) adds rw c_i c_j at (q - i, q - j): lane p's diagonal takes its
+    // own rows' c_0 terms, lane p+1's c_1 terms and lane p+2's c_2 terms, and so on
     const double a1 = rw[1] * c11, a2 = rw[2] * c21, b2 = rw[2] * c22;
     const double dg = (c0 * c0 * rw[0] + rw[1] * c10 * c10) + rw[2] * c20 * c20;
-    const double b0 = (dg + LN::shl2(a1 * c11 + a2 * c21) + LN::shl4(b2 * c22)) + s;
-    const double bp2 = LN::shl2(a1 * c10 + a2 * c20) + LN::shl4(b2 * c21);  // entry (p, p+2)
-    const double bp4 = LN::shl4(b2 * c20);                                   // entry (p, p+4)
-    const double bm2 = LN::shr2(bp2), bm4 = LN::shr4(bp4);  // symmetric: (p, p-2) = lane p-2's (., +2)
+    const double b0 = (dg + LN::shl1(a1 * c11 + a2 * c21) + LN::shl2(b2 * c22)) + s;
+    const double bp1 = LN::shl1(a1 * c10 + a2 * c20) + LN::shl2(b2 * c21);  // entry (p, p+1)
+    const double bp2 = LN::shl2(b2 * c20);                                   // entry (p, p+2)
+    const double bm1 = LN::shr1(bp1), bm2 = LN::shr2(bp2);  // symmetric: (p, p-1) = lane p-1's (., +1)
     const bool live = ln < n;
     if constexpr (kPackedP<N>) {
-      // lower band entries only: lane p adds into (p, p - 4), (p, p - 2), (p, p); the upper ones
-      // (p, p + 2), (p, p + 4) are lanes p + 2 / p + 4's (p + 2, p), (p + 4, p) (the same words)
+      // lower band entries only: lane p adds into (p, p - 2), (p, p - 1), (p, p); the upper ones
+      // (p, p + 1), (p, p + 2) are lanes p + 1 / p + 2's (p + 1, p), (p + 2, p) (the same words)
       const int Ti = (ln * (ln + 1)) / 2;
       double* rowp = P + Ti + ln;
       const double* bo = band + ln;
       lds_sync();
       if (live) {
-        if (ln >= 4) rowp[-4] = bo[0 * n] + bm4;
-        if (ln >= 2) rowp[-2] = bo[1 * n] + bm2;
+        if (ln >= 2) rowp[-2] = bo[0 * n] + bm2;
+        if (ln >= 1) rowp[-1] = bo[1 * n] + bm1;
         rowp[0] = bo[2 * n] + b0;
       }
       lds_sync();
@@ -239,22 +250,22 @@ struct Ctx {
       if (l2 < n) {
         double* rp = P + (l2 * (l2 + 1)) / 2 + l2;
         const double* bp = band + l2;
-        if (l2 >= 4) rp[-4] = bp[0 * n];
-        if (l2 >= 2) rp[-2] = bp[1 * n];
+        if (l2 >= 2) rp[-2] = bp[0 * n];
+        if (l2 >= 1) rp[-1] = bp[1 * n];
         rp[0] = bp[2 * n];
       }
       lds_sync();
     } else if constexpr (n >= 8) {
-      // entry (ln, ln - 4) (positive immediate offsets) and the saved originals, saved by setup_qp
-      double* rowp = P + ln * (kPS + 1) - 4;
+      // entry (ln, ln - 2) (positive immediate offsets) and the saved originals, saved by setup_qp
+      double* rowp = P + ln * (kPS + 1) - 2;
       const double* bo = band + ln;
       lds_sync();
       if (live) {
-        rowp[0] = bo[0 * n] + bm4;
-        rowp[2] = bo[1 * n] + bm2;
-        rowp[4] = bo[2 * n] + b0;
-        rowp[6] = bo[3 * n] + bp2;
-        rowp[8] = bo[4 * n] + bp4;
+        rowp[0] = bo[0 * n] + bm2;
+        rowp[1] = bo[1 * n] + bm1;
+        rowp[2] = bo[2 * n] + b0;
+        rowp[3] = bo[3 * n] + bp1;
+        rowp[4] = bo[4 * n] + bp2;
       }
       lds_sync();
       // lanes >= n: the zero padding column, so their rows are exactly zero (from the opaque lane
@@ -270,13 +281,13 @@ struct Ctx {
       int l2 = lane;
       asm volatile("" : "+v"(l2));
       if (l2 < n) {
-        double* rp = P + l2 * (kPS + 1) - 4;
+        double* rp = P + l2 * (kPS + 1) - 2;
         const double* bp = band + l2;
         rp[0] = bp[0 * n];
-        rp[2] = bp[1 * n];
-        rp[4] = bp[2 * n];
-        rp[6] = bp[3 * n];
-        rp[8] = bp[4 * n];
+        rp[1] = bp[1 * n];
+        rp[2] = bp[2 * n];
+        rp[3] = bp[3 * n];
+        rp[4] = bp[4 * n];
       }
       lds_sync();
     } else {
@@ -286,10 +297,10 @@ struct Ctx {
         constexpr int j = decltype(jc)::value;
         double t = 0.0;
         if (j == ln) t = b0;
+        if (j == ln + 1) t = bp1;
+        if (j + 1 == ln) t = bm1;
         if (j == ln + 2) t = bp2;
         if (j + 2 == ln) t = bm2;
-        if (j == ln + 4) t = bp4;
-        if (j + 4 == ln) t = bm4;
         const double pv = P[j * kPS + c];
         r[j] = live ? pv + t : 0.0;
       });
@@ -396,17 +407,18 @@ struct Ctx {
   // the active set.  false (inverse untouched) when 1 + delta c'u is not safely positive.
   __device__ __forceinline__ bool rank1(int tau, int l, double delta) {
     const int lu = LN::uniform(l);
-    // the row's coefficients on the variables lu, lu-2, lu-4 (lane lu's c)
+    // the row's coefficients on the variables lu, lu-1, lu-2 (lane lu's c; zero where they would
+    // reach into the other block)
     const double k0 = LN::readv(tau == 0 ? c0 : (tau == 1 ? c10 : c20), lu);
-    const double k1 = lu >= 2 ? LN::readv(tau == 1 ? c11 : (tau == 2 ? c21 : 0.0), lu) : 0.0;
-    const double k2 = lu >= 4 ? LN::readv(tau == 2 ? c22 : 0.0, lu) : 0.0;
+    const double k1 = lu >= 1 ? LN::readv(tau == 1 ? c11 : (tau == 2 ? c21 : 0.0), lu) : 0.0;
+    const double k2 = lu >= 2 ? LN::readv(tau == 2 ? c22 : 0.0, lu) : 0.0;
     // u = A^{-1} c: c has at most three entries, so u is three columns of the inverse -- by
-    // symmetry the lane's own registers r[lu], r[lu-2], r[lu-4] (A^{-1}[i][j] = -r_i[j])
+    // symmetry the lane's own registers r[lu], r[lu-1], r[lu-2] (A^{-1}[i][j] = -r_i[j])
     double u = k0 * pick<0, n>(lu);
     MPCQP_MARK("pol.rank1");
-    if (lu >= 2) u += k1 * pick<0, n>(lu - 2);
+    if (lu >= 1) u += k1 * pick<0, n>(lu - 1);
     MPCQP_MARK("pol.rank1");
-    if (lu >= 4) u += k2 * pick<0, n>(lu - 4);
+    if (lu >= 2) u += k2 * pick<0, n>(lu - 2);
     MPCQP_MARK("pol.rank1");
     u = act ? -u : 0.0;
     // u through LDS (the sweep's buffer), as the sweep broadcasts its pivot columns: the three entries
@@ -414,14 +426,14 @@ struct Ctx {
     // its one-stage register broadcast, as its sweep)
     double w[4], cu;
     if constexpr (kRegBcast) {
-      cu = (k0 * LN::readv(u, lu) + k1 * LN::readv(u, lu >= 2 ? lu - 2 : 0)) + k2 * LN::readv(u, lu >= 4 ? lu - 4 : 0);
+      cu = (k0 * LN::readv(u, lu) + k1 * LN::readv(u, lu >= 1 ? lu - 1 : 0)) + k2 * LN::readv(u, lu >= 2 ? lu - 2 : 0);
     } else {
       int ln = lane;
       asm volatile("" : "+v"(ln));
       lds_sync();
       colb[ln] = u;
       lds_sync();
-      cu = (k0 * colb[lu] + k1 * colb[lu >= 2 ? lu - 2 : 0]) + k2 * colb[lu >= 4 ? lu - 4 : 0];
+      cu = (k0 * colb[lu] + k1 * colb[lu >= 1 ? lu - 1 : 0]) + k2 * colb[lu >= 2 ? lu - 2 : 0];
       Unroll<0, kNW>::run([&](auto cc) {
         constexpr int c = decltype(cc)::value;
         w[c] = colb[16 * c + (ln & 15)];
@@ -528,9 +540,9 @@ struct ServeWin {
 // the parameter block only) receives the solver state for inspection.
 // Variables W = (v_1, delta_0, v_2, delta_1, ...) (a_k = (v_{k+1} - v_k)/dt: a bijective affine
 // change of the reference's U, same optimum).  Row slots owned by lane p (p < n = 2N):
-//   slot 0: v row (p even): v_{p/2+1}                                  (mpc_controller.py:81-82,115-116)
-//   slot 1: input row        a_{p/2} or delta_{p/2}                    (:83-86)
-//   slot 2: rate row         U_p - U_{p-2} (u_prev at k = 0)           (:89-106)
+//   slot 0: v row (speed lanes p < N): v_{p+1}                         (mpc_controller.py:81-82,115-116)
+//   slot 1: input row        a_k or delta_k (k = p mod N)              (:83-86)
+//   slot 2: rate row         U_k - U_{k-1} (u_prev at k = 0)           (:89-106)
 // the constant parts (v_0 = x0[3], u_prev) moved into the bounds.
 template <int N, class Win, bool Pair = false>
 __device__ __forceinline__ bool setup_qp(const mpcqp_params& p, int b, const double* __restrict__ model,
@@ -544,8 +556,9 @@ __device__ __forceinline__ bool setup_qp(const mpcqp_params& p, int b, const dou
   constexpr int S = model_stride(N);
   const int lane = win.lane();
   const bool act = lane < n;
-  const bool even = act && ((lane & 1) == 0);
-  const int cc = lane & 1;  // 0 = acceleration, 1 = steering
+  const bool even = act && lane < N;  // the speed block
+  const int cc = lane >= N ? 1 : 0;   // 0 = acceleration (speed variable), 1 = steering
+  const int kv = lane - cc * N;       // the step k of the lane's variable (v_{k+1} or delta_k)
   const double dt = p.dt;
   Stamps T, T2;
   T2.begin();
@@ -595,15 +608,18 @@ __device__ __forceinline__ bool setup_qp(const mpcqp_params& p, int b, const dou
     for (int e = lane; e < 4 * kBT; e += LN::kLanes) {
       const int kind = e / kBT, d = e % kBT - (n - 1);
       double v = 0.0;
+      // column v_{j+1} (lane j): rows v_j, v_{j+1}, v_{j+2} at d = -1, 0, 1, delta_j at N, delta_{j+1}
+      // at N + 1; column delta_j (lane N + j): rows v_{j+1} at -N, v_j at -N - 1.  The last speed
+      // (kind 2) has no a_{j+1}: no v_{j+2} row (d = 1 would be delta_0) and no delta_{j+1} row.
       if (kind == 0 || kind == 2) {  // speed column (kind 2: the last one)
         if (d == 0) v = kind == 0 ? 2.0 * r00 : r00;
-        if (d == 2 || d == -2) v = -r00;
-        if (d == 1) v = r10;
-        if (d == 3) v = -r10;
+        if (d == -1 || (d == 1 && kind == 0)) v = -r00;
+        if (d == N) v = r10;
+        if (d == N + 1 && kind == 0) v = -r10;
       } else if (kind == 1) {  // steering column
         if (d == 0) v = r11;
-        if (d == -1) v = r10;
-        if (d == -3) v = -r10;
+        if (d == -N) v = r10;
+        if (d == -N - 1) v = -r10;
       }
       (&sm.bt[0][0])[e] = v;
     }
@@ -672,7 +688,7 @@ __device__ __forceinline__ bool setup_qp(const mpcqp_params& p, int b, const dou
       // s0 = fma(k, X0[m] - o0, b0) (s1 alike), s2 = fma(kg, X2[m], c2), s3 = fma(kg, X3[m], c3), each
       // gated to 0 before the column's first step: the values of the case analysis, exactly.
       const bool gcol = lane == n;
-      const int j = lane >> 1;
+      const int j = kv;
       const double sj = gcol ? 1.0 : si[j];
       const double pa0 = gcol ? 0.0 : sm.pre[0][j + 1], pg0 = gcol ? 0.0 : sm.pre[2][j + 1];
       const double bj = (!gcol && j + 1 < N) ? be[j + 1] : 0.0, ej = (!gcol && j + 1 < N) ? et[j + 1] : 0.0;
@@ -747,8 +763,8 @@ __device__ __forceinline__ bool setup_qp(const mpcqp_params& p, int b, const dou
             mu1 = w1;
             mu2 = w2;
           }
-          Pc[2 * (m - 1)] = ha;
-          Pc[2 * (m - 1) + 1] = si[m - 1] * mu2;
+          Pc[m - 1] = ha;
+          Pc[N + m - 1] = si[m - 1] * mu2;
         }
       };
       if (diag)
@@ -766,9 +782,9 @@ __device__ __forceinline__ bool setup_qp(const mpcqp_params& p, int b, const dou
       if (gcol) {  // the v_0 = x0[3] end of a_0
         const double r00 = 0.5 * (p.r[0] + p.r[0]) / (dt * dt), r10 = 0.5 * (p.r[2] + p.r[1]) / dt;
         sm.g[0] += -x0[3] * r00;
-        sm.g[1] += -x0[3] * r10;
+        sm.g[N] += -x0[3] * r10;
       }
-      const int kind = gcol ? 3 : (cc == 1 ? 1 : (lane + 2 < n ? 0 : 2));
+      const int kind = gcol ? 3 : (cc == 1 ? 1 : (lane + 1 < N ? 0 : 2));
       const double* tb = &sm.bt[kind][n - 1 - lane];
 #pragma unroll
       for (int i = 0; i < n; ++i) Pc[i] += tb[i];
@@ -798,7 +814,7 @@ __device__ __forceinline__ bool setup_qp(const mpcqp_params& p, int b, const dou
     const double r11 = 0.5 * (p.r[3] + p.r[3]);
 #pragma nounroll
     for (int gpass = 0; gpass < 2; ++gpass) {
-      const int j = lane >> 1;
+      const int j = kv;
       const bool gcol = gpass == 1;
       const double sj = gcol ? 0.0 : si[j];
       const double pa0 = gcol ? 0.0 : sm.pre[0][j + 1], pg0 = gcol ? 0.0 : sm.pre[2][j + 1];
@@ -850,8 +866,8 @@ __device__ __forceinline__ bool setup_qp(const mpcqp_params& p, int b, const dou
         // two conditions, not an if/else: merged into one store through a select of the two
         // addresses, the column would be addressed through a generic pointer (scratch memory)
         if (gcol && lane == 0) {
-          sm.g[2 * (m - 1)] = ha;
-          sm.g[2 * (m - 1) + 1] = hd;
+          sm.g[m - 1] = ha;
+          sm.g[N + m - 1] = hd;
         }
         if (!gcol) {
           int ln = lane;  // opaque per step: the band's compares are not hoisted out of the pass loop
@@ -859,26 +875,27 @@ __device__ __forceinline__ bool setup_qp(const mpcqp_params& p, int b, const dou
           auto band = [&](int i) -> double {  // the band entry of row i in column ln
             const int d = i - ln;
             double add = 0.0;
-            if (cc == 0) {
-              if (d == 0) add = ln + 2 < n ? 2.0 * r00 : r00;
-              if (d == 2 || d == -2) add = -r00;
-              if (d == 1) add = r10;
-              if (d == 3) add = -r10;
+            if (cc == 0) {  // the band table's values (above)
+              const bool last = ln + 1 >= N;
+              if (d == 0) add = last ? r00 : 2.0 * r00;
+              if (d == -1 || (d == 1 && !last)) add = -r00;
+              if (d == N) add = r10;
+              if (d == N + 1 && !last) add = -r10;
             } else {
               if (d == 0) add = r11;
-              if (d == -1) add = r10;
-              if (d == -3) add = -r10;
+              if (d == -N) add = r10;
+              if (d == -N - 1) add = -r10;
             }
             return add;
           };
-          Pc[2 * (m - 1)] = ha + band(2 * (m - 1));
-          Pc[2 * (m - 1) + 1] = hd + band(2 * (m - 1) + 1);
+          Pc[m - 1] = ha + band(m - 1);
+          Pc[N + m - 1] = hd + band(N + m - 1);
         }
         __builtin_amdgcn_sched_barrier(0);
       });
       if (gcol && lane == 0) {  // the v_0 = x0[3] end of a_0
         sm.g[0] += -x0[3] * r00;
-        sm.g[1] += -x0[3] * r10;
+        sm.g[N] += -x0[3] * r10;
       }
     }
     __syncthreads();
@@ -897,18 +914,19 @@ __device__ __forceinline__ bool setup_qp(const mpcqp_params& p, int b, const dou
   }
   double cmax = fmax(fmax(cmx[0], cmx[1]), fmax(cmx[2], cmx[3]));
   double lo[3], hi[3], wt[3], E[3];
-  // unscaled row coefficients (slot 1: own, 2 back; slot 2: own, 2 back, 4 back)
+  // unscaled row coefficients (slot 1: own, 1 back; slot 2: own, 1 back, 2 back): exact zeros where
+  // the variable back is a constant (v_0, u_prev) or would lie in the other block
   const double idt = 1.0 / dt, v0 = x0[3];
   double k1[2], k2[3];
   k1[0] = act ? (even ? idt : 1.0) : 0.0;
-  k1[1] = (even && lane >= 2) ? -idt : 0.0;
+  k1[1] = (even && kv >= 1) ? -idt : 0.0;
   k2[0] = act ? (even ? idt : 1.0) : 0.0;
-  k2[1] = act ? (even ? (lane >= 2 ? -2.0 * idt : 0.0) : (lane >= 3 ? -1.0 : 0.0)) : 0.0;
-  k2[2] = (even && lane >= 4) ? idt : 0.0;
+  k2[1] = act ? (even ? (kv >= 1 ? -2.0 * idt : 0.0) : (kv >= 1 ? -1.0 : 0.0)) : 0.0;
+  k2[2] = (even && kv >= 2) ? idt : 0.0;
   {
     // the rows' constant parts moved into the bounds: a_0 = (v_1 - v_0)/dt, a_1 - a_0 carries +v_0/dt
     const double ofa = lane == 0 ? v0 * idt : 0.0;
-    const double ofr = lane < 2 ? up[cc] + ofa : (lane == 2 ? -v0 * idt : 0.0);
+    const double ofr = (act && kv == 0) ? up[cc] + ofa : ((even && kv == 1) ? -v0 * idt : 0.0);
     lo[0] = even ? p.v_bounds[0] : 0.0;
     hi[0] = even ? p.v_bounds[1] : 0.0;
     wt[0] = even ? p.slack_velocity : 0.0;
@@ -939,16 +957,16 @@ __device__ __forceinline__ bool setup_qp(const mpcqp_params& p, int b, const dou
   MPCQP_MARK("setup.ruiz");
   for (int it = 0; it < p.scaling; ++it) {
     // column norms of [P; A] (first n columns of the KKT matrix): the lane's own rows and
-    // the banded rows 2 and 4 ahead
+    // the banded rows 1 and 2 ahead
     double ccol = fmax(fmax(E[0], E[1] * fabs(k1[0])), E[2] * fabs(k2[0]));
-    ccol = fmax(ccol, LN::shl2(fmax(E[1] * fabs(k1[1]), E[2] * fabs(k2[1]))));
-    ccol = fmax(ccol, LN::shl4(E[2] * fabs(k2[2])));
+    ccol = fmax(ccol, LN::shl1(fmax(E[1] * fabs(k1[1]), E[2] * fabs(k2[1]))));
+    ccol = fmax(ccol, LN::shl2(E[2] * fabs(k2[2])));
     ccol *= D;
     const double dl = act ? rsqrt(limit_scaling(fmax(cmax, ccol))) : 0.0;
     // row norms of A
-    const double Dm2 = LN::shr2(D), Dm4 = LN::shr2(Dm2);
-    const double r1 = fmax(fabs(k1[0]) * D, fabs(k1[1]) * Dm2);
-    const double r2 = fmax(fmax(fabs(k2[0]) * D, fabs(k2[1]) * Dm2), fabs(k2[2]) * Dm4);
+    const double Dm1 = LN::shr1(D), Dm2 = LN::shr1(Dm1);
+    const double r1 = fmax(fabs(k1[0]) * D, fabs(k1[1]) * Dm1);
+    const double r2 = fmax(fmax(fabs(k2[0]) * D, fabs(k2[1]) * Dm1), fabs(k2[2]) * Dm2);
     const double el0 = even ? rsqrt(limit_scaling(E[0] * D)) : 0.0;
     const double el1 = act ? rsqrt(limit_scaling(E[1] * r1)) : 0.0;
     const double el2 = act ? rsqrt(limit_scaling(E[2] * r2)) : 0.0;
@@ -1010,8 +1028,8 @@ __device__ __forceinline__ bool setup_qp(const mpcqp_params& p, int b, const dou
     lds_sync();
     if (act) {  // form()'s band addresses: save what they hold
       const double* rowp = Pb + (lane * (lane + 1)) / 2 + lane;
-      lds.solve.band[0][lane] = lane >= 4 ? rowp[-4] : 0.0;
-      lds.solve.band[1][lane] = lane >= 2 ? rowp[-2] : 0.0;
+      lds.solve.band[0][lane] = lane >= 2 ? rowp[-2] : 0.0;
+      lds.solve.band[1][lane] = lane >= 1 ? rowp[-1] : 0.0;
       lds.solve.band[2][lane] = rowp[0];
     }
   } else {
@@ -1036,7 +1054,7 @@ __device__ __forceinline__ bool setup_qp(const mpcqp_params& p, int b, const dou
       if (act) {
         const double* rowp = Pb + lane * (kPS + 1);
 #pragma unroll
-        for (int d = 0; d < 5; ++d) lds.solve.band[d][lane] = rowp[2 * d - 4];
+        for (int d = 0; d < 5; ++d) lds.solve.band[d][lane] = rowp[d - 2];
       }
     }
   }
@@ -1056,13 +1074,13 @@ __device__ __forceinline__ bool setup_qp(const mpcqp_params& p, int b, const dou
   C.D = D;
   C.cscale = cscale;
   {  // Cbar's coefficients: row scaling x row coefficient x the column scaling of the variable
-    const double Dm2 = LN::shr2(D), Dm4 = LN::shr2(Dm2);
+    const double Dm1 = LN::shr1(D), Dm2 = LN::shr1(Dm1);
     C.c0 = E[0] * D;
     C.c10 = (E[1] * k1[0]) * D;
-    C.c11 = (E[1] * k1[1]) * Dm2;
+    C.c11 = (E[1] * k1[1]) * Dm1;
     C.c20 = (E[2] * k2[0]) * D;
-    C.c21 = (E[2] * k2[1]) * Dm2;
-    C.c22 = (E[2] * k2[2]) * Dm4;
+    C.c21 = (E[2] * k2[1]) * Dm1;
+    C.c22 = (E[2] * k2[2]) * Dm2;
   }
 #pragma unroll
   for (int r = 0; r < 3; ++r) {
@@ -1072,20 +1090,22 @@ __device__ __forceinline__ bool setup_qp(const mpcqp_params& p, int b, const dou
     C.wb[r] = wb[r];
   }
   __syncthreads();
-  if (dbg) {
+  if (dbg) {  // in the reference-facing variable order (interleaved<N>)
+    const int il = interleaved<N>(lane);
     if (act)
       for (int i = 0; i < n; ++i)
-        dbg[i * n + lane] = kPackedP<N> ? lds.solve.P[tri_idx(i, lane)] : lds.solve.P[i * SolveSmem<N>::kPS + lane];
+        dbg[interleaved<N>(i) * n + il] =
+            kPackedP<N> ? lds.solve.P[tri_idx(i, lane)] : lds.solve.P[i * SolveSmem<N>::kPS + lane];
     double* lf = dbg + state_lane_off(N);
-    lf[kFq * kWave + lane] = qv;
-    lf[kFD * kWave + lane] = D;
-    lf[kFx * kWave + lane] = 0.0;
+    lf[kFq * kWave + il] = qv;
+    lf[kFD * kWave + il] = D;
+    lf[kFx * kWave + il] = 0.0;
 #pragma unroll
     for (int r = 0; r < 3; ++r) {
-      lf[(kFE0 + r) * kWave + lane] = E[r];
-      lf[(kFlo0 + r) * kWave + lane] = lo[r];
-      lf[(kFhi0 + r) * kWave + lane] = hi[r];
-      lf[(kFw0 + r) * kWave + lane] = wb[r];
+      lf[(kFE0 + r) * kWave + il] = E[r];
+      lf[(kFlo0 + r) * kWave + il] = lo[r];
+      lf[(kFhi0 + r) * kWave + il] = hi[r];
+      lf[(kFw0 + r) * kWave + il] = wb[r];
     }
     if (lane == 0) {
       double* sc = dbg + state_scal_off(N);
@@ -1485,7 +1505,7 @@ template <int N>
 __device__ __forceinline__ void admm_debug_state(double* __restrict__ dbg, bool act, double x, int flag, int it,
                                                  int nfact) {
   if (!dbg) return;
-  dbg[state_lane_off(N) + kFx * kWave + threadIdx.x] = act ? x : 0.0;
+  dbg[state_lane_off(N) + kFx * kWave + interleaved<N>(threadIdx.x)] = act ? x : 0.0;
   if (threadIdx.x == 0) {
     double* sc = dbg + state_scal_off(N);
     sc[1] = flag < 0 ? -1.0 : (flag > 0 ? 1.0 : 0.0);
@@ -1604,20 +1624,20 @@ __device__ __forceinline__ int finish_qp(const mpcqp_params& p, int b, const dou
     up0 = mb[11 * N + 8];
     up1 = mb[11 * N + 9];
   }
-  const int cc = lane & 1;
-  const double W = act ? C.D * x : 0.0;  // v_{j+1} on lane 2j, delta_j on lane 2j+1
+  const int cc = lane >= N ? 1 : 0;
+  const int kv = lane - cc * N;
+  const double W = act ? C.D * x : 0.0;  // v_{j+1} on lane j, delta_j on lane N + j
   const double dt = p.dt;
-  const double Wm2 = LN::shr2(W);
-  const double U = !act ? 0.0 : (cc == 1 ? W : (W - (lane == 0 ? x03 : Wm2)) / dt);
-  const double sj_all = LN::shfl(m_si, lane >> 1);
+  const double Wm1 = LN::shr1(W);       // lane k <- v_k (k = 1..N)
+  const double U = !act ? 0.0 : (cc == 1 ? W : (W - (lane == 0 ? x03 : Wm1)) / dt);
+  const double sj_all = LN::shfl(m_si, cc ? kv : 0);
   const double sj = act ? sj_all : 0.0;
-  // psi_{j+1} on lane 2j+1
+  // psi_{j+1} - psi_0 on lane N + j
   const double sacc = LN::scan((act && cc == 1) ? sj * U : 0.0, lane);
   // lane k <- (psi_k, v_k)
-  const int srcv = lane == 0 ? 0 : 2 * (lane - 1);
-  const double vk_s = LN::shfl(W, srcv < LN::kLanes ? srcv : 0);
-  const double pk_s = LN::shfl(sacc, (srcv + 1) < LN::kLanes ? srcv + 1 : 0);
-  const double vk = lane == 0 ? x03 : vk_s;
+  const int srcp = lane == 0 ? 0 : N + lane - 1;
+  const double pk_s = LN::shfl(sacc, srcp < LN::kLanes ? srcp : 0);
+  const double vk = lane == 0 ? x03 : Wm1;
   const double pk = lane == 0 ? x02 : x02 + pk_s;
   double t0 = 0.0, t1 = 0.0;
   if (lane < N) {
@@ -1635,16 +1655,17 @@ __device__ __forceinline__ int finish_qp(const mpcqp_params& p, int b, const dou
     Xb[3 * (N + 1) + lane] = vk;
   }
   Uout = U;
-  if (Uo && act) Uo[(size_t)b * n + cc * N + (lane >> 1)] = U;
-  if (u0o && lane < 2) u0o[(size_t)b * 2 + lane] = U;
-  const double Um2 = LN::shr2(U);
+  if (Uo && act) Uo[(size_t)b * n + lane] = U;  // U[c][k] at c * N + k: the lane itself
+  if (u0o && act && kv == 0) u0o[(size_t)b * 2 + cc] = U;
+  const double Um1 = LN::shr1(U);
   if (activeo) {
     uint8_t* ab = activeo + (size_t)b * (5 * N + 1);
     if (lane <= N) ab[lane] = vk > p.v_bounds[1] ? 2 : (vk < p.v_bounds[0] ? 1 : 0);
-    if (act) {
-      ab[N + 1 + lane] = U > p.u_bounds[2 * cc + 1] ? 2 : (U < p.u_bounds[2 * cc] ? 1 : 0);
-      const double d = U - (lane < 2 ? (cc ? up1 : up0) : Um2);
-      ab[3 * N + 1 + lane] = d > p.du_bounds[2 * cc + 1] ? 2 : (d < p.du_bounds[2 * cc] ? 1 : 0);
+    if (act) {  // input and rate rows in the reference-facing order (a_0, delta_0, a_1, ...)
+      const int il = interleaved<N>(lane);
+      ab[N + 1 + il] = U > p.u_bounds[2 * cc + 1] ? 2 : (U < p.u_bounds[2 * cc] ? 1 : 0);
+      const double d = U - (kv == 0 ? (cc ? up1 : up0) : Um1);
+      ab[3 * N + 1 + il] = d > p.du_bounds[2 * cc + 1] ? 2 : (d < p.du_bounds[2 * cc] ? 1 : 0);
     }
   }
   T3.end(0);
@@ -1663,7 +1684,7 @@ __device__ __forceinline__ int finish_qp(const mpcqp_params& p, int b, const dou
 
 // One QP through setup -> ADMM (+ early polish attempts) -> final polish -> outputs on the calling
 // wave, for the fused fleet loop (k_fleet_loop; no debug state): returns the status, Ulane = the
-// lane's U entry (lane 0/1: u0).  k_solve runs the same driver inline (below).
+// lane's U entry (lanes 0 and N: u0).  k_solve runs the same driver inline (below).
 template <int N, class Win, bool Pair = false>
 __device__ __forceinline__ int solve_one(const mpcqp_params& p, int b, const double* __restrict__ model,
                                          const double* __restrict__ in_x0, const double* __restrict__ in_ref,
@@ -2002,7 +2023,7 @@ __global__ __launch_bounds__(kWave, kSolveWavesPerEU<N>) void k_fleet_loop(const
       break;
     }
     // k_fleet_advance (every lane computes the same values)
-    const double a = LN::readv(U, 0), delta = LN::readv(U, 1);
+    const double a = LN::readv(U, 0), delta = LN::readv(U, N);  // u0: lanes 0 and N
     double x[4] = {ls[0], ls[1], ls[2], ls[3]}, xn[4];
     plant(x, a, delta, P[0].dt, P[0].wheelbase_px, xn);
     if (lane == 0) {
