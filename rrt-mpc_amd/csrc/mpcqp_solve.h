@@ -478,13 +478,16 @@ struct Ctx {
       vbcast(act ? v : 0.0, w);
     else
       vbcast(v, w);
-    // two chains: a dependent f64 FMA's latency (~9 cycles) is under two issue slots (~5.5 each)
-    double a[2] = {0.0, 0.0};
+    // three chains: a dependent f64 FMA's latency (~9 cycles) is under two issue slots (~5.5 each),
+    // and a DPP FMA that reads an accumulator written two instructions earlier needs a wait state
+    // (two chains: an s_nop per pair; three chains none): config 2 +1.9 %, the config-4 shard +1.0 %,
+    // B=1 +1.1 % over two chains, config 3 level (profiles/r05_t_ab_three_chain_invmul.json)
+    double a[3] = {0.0, 0.0, 0.0};
     Unroll<0, n>::run([&](auto jc) {
       constexpr int j = decltype(jc)::value;
-      fmac_bc<j % 16>(a[j % 2], w[j / 16], r[j]);
+      fmac_bc<j % 16>(a[j % 3], w[j / 16], r[j]);
     });
-    return -(a[0] + a[1]);
+    return -((a[0] + a[1]) + a[2]);
   }
 };
 
