@@ -28,7 +28,7 @@ NAMES = {0: "admm.form", 1: "admm.sweep", 2: "admm.iteration", 3: "admm.check", 
          8: "polish.form", 9: "polish.sweep", 10: "polish.solve", 11: "polish.linesearch", 12: "polish.total",
          13: "finish.outputs", 22: "qp.total",
          16: "setup.load_prefix", 17: "setup.condense", 18: "setup.unscaled", 19: "setup.ruiz", 20: "setup.write",
-         21: "setup.total"}
+         21: "setup.total", 26: "setup.write.finite_model", 27: "setup.write.pbar", 28: "setup.write.context"}
 
 
 def main() -> None:
