@@ -30,14 +30,14 @@ def build():
 
 
 def run(Ns):
-    os.environ["MPCQP_LIB"] = str(LIB)
+    os.environ.setdefault("MPCQP_LIB", str(LIB))
     sys.path.insert(0, str(ROOT / "rrt-mpc_amd"))
     import torch
     from mpcqp import _lib, scenarios
     from mpcqp.config import MPCConfig
     from mpcqp.control.mpc_controller import BatchedMPCController
 
-    L = ctypes.CDLL(str(LIB))
+    L = ctypes.CDLL(os.environ["MPCQP_LIB"])
     out = {}
     for N in Ns:
         b = scenarios.config3(4096, horizon=N)
