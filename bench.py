@@ -196,6 +196,15 @@ def reduce_stats(ctx: DistContext, elapsed: float, sums: List[float]) -> Tuple[f
     return float(t.item()), [float(v) for v in s.cpu().tolist()]
 
 
+def gather_scalar(ctx: DistContext, v: float) -> List[float]:
+    """Every rank's value of a per-rank scalar, in rank order (one all_gather; [v] at world 1): the
+    per-rank elapsed times beside the MAX over ranks, so shard imbalance is visible."""
+    import torch
+
+    t = torch.tensor([float(v)], dtype=torch.float64, device=ctx._cdev())
+    return [float(p.item()) for p in ctx.all_gather(t)]
+
+
 def gather_rows(ctx: DistContext, t, counts: List[int]):
     """All ranks' shards of a row-distributed tensor, concatenated in rank order (shards of
     unequal length are padded to the largest for the collective)."""
@@ -344,15 +353,21 @@ def cpu_baseline(params, x0, ref, u_prev, seconds: float, settings=None) -> dict
         out1 = cpu_solver.cpu_solve(params, x0[:256], ref[:256], u_prev[:256], nthreads=1, **(settings or {}))
         n1 += int((out1["status"] == 1).sum())
     dt1 = time.perf_counter() - t1
-    # every core this process may run on (SURVEY.md 8(d) "the host's cores"): a shorter slice, since
-    # on the GPU box those cores are the whole node's, shared with its other GPUs' host work
-    na, ta = 0, time.perf_counter()
-    while True:
-        outa = cpu_solver.cpu_solve(params, x0, ref, u_prev, nthreads=visible, **(settings or {}))
-        na += int((outa["status"] == 1).sum())
-        if time.perf_counter() - ta >= min(5.0, max(1.0, seconds / 2)):
-            break
-    dta = time.perf_counter() - ta
+    # every core this process may use (SURVEY.md 8(d) "the host's cores"): the affinity mask capped by
+    # the cgroup's CPU quota (on the GPU box the mask shows the whole node, 256 cores, while the job's
+    # quota is 16: more threads than that only oversubscribe the quota)
+    quota = cgroup_cpu_quota()
+    all_threads = max(1, min(visible, int(np.ceil(quota)))) if quota else visible
+    if all_threads == threads:  # the share above is already every usable core
+        na, dta = solved, dt
+    else:
+        na, ta = 0, time.perf_counter()
+        while True:
+            outa = cpu_solver.cpu_solve(params, x0, ref, u_prev, nthreads=all_threads, **(settings or {}))
+            na += int((outa["status"] == 1).sum())
+            if time.perf_counter() - ta >= min(5.0, max(1.0, seconds / 2)):
+                break
+        dta = time.perf_counter() - ta
     return {
         "value": solved / dt,
         "unit": "QP/s",
@@ -362,15 +377,16 @@ def cpu_baseline(params, x0, ref, u_prev, seconds: float, settings=None) -> dict
         "host_cores_visible": visible,
         "value_1core": n1 / dt1,
         "value_all_cores": na / dta,
-        "threads_all_cores": visible,
-        "cgroup_cpu_quota_cores": cgroup_cpu_quota(),
+        "threads_all_cores": all_threads,
+        "cgroup_cpu_quota_cores": quota,
         "cpu_model": _cpu_model(),
         "sample": f"{done} QPs ({done // len(x0)} passes over this rank's batch) in {dt:.1f} s on {threads} "
                   f"OpenMP threads: the host's CPU share of this GPU (OMP_NUM_THREADS; {visible} cores are "
                   f"visible to the process, shared with the node's other GPUs); C restatement of the same "
                   f"ADMM+polish algorithm (oracle/mpcqp_cpu.c); value_1core: one thread on 256 QPs; "
-                  f"value_all_cores: all {visible} visible cores on the same batch ({dta:.1f} s; above the "
-                  f"cgroup's CPU quota, cgroup_cpu_quota_cores, the threads oversubscribe it)",
+                  f"value_all_cores: every core this process may use -- the {visible} visible cores capped by "
+                  f"the cgroup CPU quota ({quota if quota else 'none'}) -- {all_threads} threads on the same "
+                  f"batch ({dta:.1f} s{'; the same run as value' if all_threads == threads else ''})",
     }
 
 
@@ -806,6 +822,7 @@ def strong_leg(ctx: DistContext, steps: int, warmup: int, method: str, extra: di
 
         elapsed = timed_steps(step, steps, warmup, ctx, lambda: torch.cuda.synchronize(ctx.device))
         status = ctrl._status[:B]
+        rank_s = gather_scalar(ctx, elapsed)
         T, (solved,) = reduce_stats(ctx, elapsed, [float((status == 1).sum().item())])
         g = {k: gather_rows(ctx, t[:B], counts).cpu().numpy() for k, t in
              (("status", ctrl._status), ("U", ctrl._U), ("active", ctrl._active))}
@@ -821,6 +838,8 @@ def strong_leg(ctx: DistContext, steps: int, warmup: int, method: str, extra: di
             "global_batch": total,
             "batch_per_gpu": counts,
             "ms_per_step": 1e3 * T / steps,
+            # each rank's own elapsed time per step (the line's ms_per_step is their MAX): shard imbalance
+            "rank_ms_per_step": [1e3 * e / steps for e in rank_s],
             "steps": steps,
             "warmup": warmup,
             "solved_fraction": solved / total,
@@ -948,6 +967,7 @@ def main() -> int:
     status = ctrl._status[:B].cpu().numpy()
     iters = ctrl._iters[:B].cpu().numpy()
     flops = qp_flops(N, iters, scaling=int(ctrl._cparams.scaling), check=int(ctrl._cparams.check_termination))
+    rank_s = gather_scalar(ctx, elapsed)
     T, (solved_all, flops_all, admm_all, pol_all) = reduce_stats(
         ctx, elapsed, [float((status == 1).sum()), float(flops.sum()), float(iters[:, 0].sum()),
                        float(iters[:, 1].sum())])
@@ -977,6 +997,8 @@ def main() -> int:
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": ms_per_step,
+            # each rank's own elapsed time per step (ms_per_step is their MAX): shard imbalance
+            "rank_ms_per_step": [1e3 * e / args.steps for e in rank_s],
             "higher_is_better": True,
             "scaling": "strong" if strong else "weak",
             "vs_baseline": None,
@@ -1066,10 +1088,19 @@ def main() -> int:
             out["config1"] = config1_closed_loop()
         if world == 1 and not args.no_config5 and args.config == "config3" and not args.horizon:
             out["config5"] = config5_swarm()
-        print(json.dumps(out), flush=True)
+        if world == 1:
+            print(json.dumps(out), flush=True)
     ctx.barrier()
     ctrl.close()
     ctx.close()
+    if rank == 0 and world > 1:
+        # the N-rank line carries the CPU baseline too: rank 0 times it after every rank's GPU legs and
+        # collectives are over (the other ranks are leaving, so it does not share their host cores)
+        if args.cpu_seconds > 0:
+            out["cpu_baseline"] = cpu_baseline(params, x0, ref, u_prev, args.cpu_seconds, settings=extra)
+            out["cpu_baseline"]["note"] = (f"measured on rank 0 after the {world} ranks' timed legs: the host CPU "
+                                           f"share of one GPU (threads) and one core, on rank 0's shard")
+        print(json.dumps(out), flush=True)
     return 0
 
 

@@ -200,13 +200,17 @@ int mpcqp_solve_staged(mpcqp_ws* ws);
  * workspace's stream that solves the staged QP each time this function raises a request in a
  * mailbox of mapped host memory, and publishes completion there (the call spins on it).  The wave
  * leaves after 2 ms without a request, at mpcqp_set_params and at mpcqp_destroy; the next call
- * starts it again.  One server is resident per device: a request on another workspace of the same
- * device first stops the live one (a switch costs one stop and one launch).  The workspace's stream
- * has the device's highest priority, so its hardware queue is not one that default-priority streams
- * (torch's) share.  While a wave is resident, a device-wide synchronisation (hipDeviceSynchronize)
- * waits for it to go idle.  A request unanswered for 30 s returns MPCQP_E_DEVICE and the workspace
- * refuses later B = 1 requests.  Horizons without the one-wave kernel (N > 32, reproducible, debug
- * builds) run mpcqp_solve_staged.  Not thread-safe per workspace (the closed loop is sequential). */
+ * starts it again.  One server is resident per device while its workspaces are used from one thread:
+ * a request on another workspace of the same device first stops the live one (a switch costs one stop
+ * and one launch).  Distinct workspaces may be served from distinct threads at the same time: each call
+ * holds its own workspace's lock, and a workspace busy in a call on another thread keeps its wave (two
+ * resident waves until one goes idle) instead of being stopped.  The workspace's stream has the
+ * device's highest priority, so its hardware queue is not one that default-priority streams (torch's)
+ * share.  While a wave is resident, a device-wide synchronisation (hipDeviceSynchronize) waits for it
+ * to go idle.  A request unanswered for 30 s returns MPCQP_E_DEVICE and the workspace refuses later
+ * B = 1 requests; it has told its wave to leave, and mpcqp_destroy of that workspace waits until the
+ * wave has left (it may still be queued).  Horizons without the one-wave kernel (N > 32, reproducible,
+ * debug builds) run mpcqp_solve_staged.  Not thread-safe per workspace (the closed loop is sequential). */
 int mpcqp_solve_served(mpcqp_ws* ws);
 
 /* Two QPs per wave for horizons N <= 15 (2N <= 30 variables: a one-wave QP leaves half its lanes on

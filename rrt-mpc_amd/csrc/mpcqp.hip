@@ -447,9 +447,9 @@ int mpcqp_solve_staged(mpcqp_ws* ws) {
 static std::mutex g_serve_mu;
 static mpcqp_ws* g_server[64] = {};
 
-// The B = 1 server (k_serve): ends a live server wave (kServeStop) and waits for it.
-static void serve_stop(mpcqp_ws* ws) {
-  if (!ws) return;
+// The B = 1 server (k_serve): ends a live server wave (kServeStop) and waits for it.  The caller
+// holds ws->serve_mu.
+static void serve_stop_locked(mpcqp_ws* ws) {
   {
     std::lock_guard<std::mutex> lk(g_serve_mu);
     if (g_server[ws->device & 63] == ws) g_server[ws->device & 63] = nullptr;
@@ -463,6 +463,11 @@ static void serve_stop(mpcqp_ws* ws) {
   ws->serve_seq = __atomic_load_n(&box->done, __ATOMIC_ACQUIRE);
   ws->serve_live = false;
 }
+static void serve_stop(mpcqp_ws* ws) {
+  if (!ws) return;
+  std::lock_guard<std::mutex> own(ws->serve_mu);
+  serve_stop_locked(ws);
+}
 
 int mpcqp_solve_served(mpcqp_ws* ws) {
   if (!ws) return fail(MPCQP_E_ARG, "null ws");
@@ -471,13 +476,27 @@ int mpcqp_solve_served(mpcqp_ws* ws) {
     return fail(MPCQP_E_DEVICE, "B=1 server: an earlier request went unanswered; this workspace is unusable");
   const mpcqp::serve_t launch = mpcqp::server(ws->p);
   if (!launch) return mpcqp_solve_staged(ws);  // long horizons, reproducible or debug builds
+  // this workspace's server state is ours for the whole call; another workspace's wave on this device
+  // is stopped only when its own lock is free (try-lock, taken under g_serve_mu so that workspace cannot
+  // be destroyed in between): a workspace busy in its own served call on another thread keeps its wave,
+  // which leaves 2 ms after its last request -- two resident waves for that while, never a stop
+  // that overwrites a pending request
+  std::unique_lock<std::mutex> own(ws->serve_mu);
   mpcqp_ws* other = nullptr;
+  std::unique_lock<std::mutex> other_lk;
   {
     std::lock_guard<std::mutex> lk(g_serve_mu);
     other = g_server[ws->device & 63];
+    if (other && other != ws) {
+      other_lk = std::unique_lock<std::mutex>(other->serve_mu, std::try_to_lock);
+      if (!other_lk.owns_lock()) other = nullptr;
+    } else {
+      other = nullptr;
+    }
     g_server[ws->device & 63] = ws;
   }
-  if (other && other != ws) serve_stop(other);
+  if (other) serve_stop_locked(other);
+  if (other_lk.owns_lock()) other_lk.unlock();
   if (!ws->serve_box) {
     int cur = -1;
     hipError_t e = hipGetDevice(&cur);
@@ -552,6 +571,10 @@ int mpcqp_solve_served(mpcqp_ws* ws) {
         __atomic_store_n(&box->req, mpcqp::kServeStop, __ATOMIC_RELEASE);
         ws->serve_live = false;
         ws->serve_broken = true;
+        {  // no other workspace's request stops (or counts on) this wave any more
+          std::lock_guard<std::mutex> lk(g_serve_mu);
+          if (g_server[ws->device & 63] == ws) g_server[ws->device & 63] = nullptr;
+        }
         return fail(MPCQP_E_DEVICE, "B=1 server: no answer within 30 s");
       }
     }

@@ -8,6 +8,7 @@
 #include <cstdint>
 #include <cstdio>
 #include <cstring>
+#include <mutex>
 #include <new>
 #include <string>
 #include <type_traits>
@@ -534,6 +535,10 @@ struct mpcqp_ws {
   bool serve_broken;  // a request went unanswered (30 s): the workspace refuses B = 1 requests
   int serve_fault;    // mpcqp_debug_serve_fault: 1 = refuse the next server launch
   std::chrono::steady_clock::time_point serve_last;  // the last completed request (host clock)
+  // guards the server fields above: held by mpcqp_solve_served for its whole call, by set_params /
+  // destroy around their stop, and try-locked by another workspace's served call that would stop this
+  // workspace's wave (it skips the stop while this one is busy)
+  std::mutex serve_mu;
   // two QPs per wave for N <= 15 (MPCQP_PAIR_*, mpcqp_set_pairing)
   int pairing;
   int cus;  // the device's compute units (queried once at mpcqp_create; 0 if unknown)

@@ -1086,7 +1086,8 @@ __device__ __forceinline__ void mid_finish(const mpcqp_params& p, int b, Mid<NT>
       ab[3 * N + 1 + i] = d > p.du_bounds[2 * cc + 1] ? 2 : (d < p.du_bounds[2 * cc] ? 1 : 0);
     }
   }
-  // states on wave 0 (N + 1 <= 64 lanes): lane k <- (psi_k, v_k), positions by the LTV recursion
+  // states on wave 0 (lanes 0..min(N, 63)): lane k <- (psi_k, v_k), positions by the LTV recursion; at
+  // N = 64 the last state row (k = 64) is written from lane 63's inclusive sums (below)
   if (threadIdx.x < kWave) {
     const int k = threadIdx.x;
     const double x00 = mdl[11 * N + 4], x01 = mdl[11 * N + 5], x02 = mdl[11 * N + 6];

@@ -787,8 +787,10 @@ __device__ __forceinline__ bool setup_qp(const mpcqp_params& p, int b, const dou
         sm.g[0] += -x0[3] * r00;
         sm.g[N] += -x0[3] * r10;
       }
+      // the g column (lane n) reads kind 3 (all zeros) from offset 0: n - 1 - n would be the last word
+      // of bt[2], not a zero
       const int kind = gcol ? 3 : (cc == 1 ? 1 : (lane + 1 < N ? 0 : 2));
-      const double* tb = &sm.bt[kind][n - 1 - lane];
+      const double* tb = &sm.bt[kind][gcol ? 0 : n - 1 - lane];
 #pragma unroll
       for (int i = 0; i < n; ++i) Pc[i] += tb[i];
     }

@@ -50,11 +50,12 @@ def _worker(rank, world, port, total, out_dir):
 
     elapsed = bench.timed_steps(step, 2, 1, ctx)
     T, (solved,) = bench.reduce_stats(ctx, elapsed + rank, [float((res["status"] == 1).sum())])
+    per_rank = bench.gather_scalar(ctx, 10.0 * rank + 0.5)
     g = {k: bench.gather_rows(ctx, torch.from_numpy(res[k]), counts).numpy() for k in ("u0", "status", "U", "active")}
     if rank == 0:
         chk = bench.spot_check(params, batch.x0, batch.ref, batch.u_prev, g["U"], g["active"], g["status"],
                                np.arange(0, total, 5))
-        np.savez(Path(out_dir) / "dist.npz", T=T, elapsed=elapsed, solved=solved, u0=g["u0"], status=g["status"],
+        np.savez(Path(out_dir) / "dist.npz", T=T, elapsed=elapsed, per_rank=np.array(per_rank), solved=solved, u0=g["u0"], status=g["status"],
                  U=g["U"], err=chk["max_rel_err_U"], mism=chk["active_set_mismatches"] + chk["status_mismatches"])
     ctx.barrier()
     ctx.close()
@@ -76,6 +77,8 @@ def test_sharded_solve_matches_single_process(tmp_path, world, total):
     d = np.load(tmp_path / "dist.npz")
     # MAX over ranks: rank r reported its elapsed time + r seconds
     assert float(d["T"]) >= max(float(d["elapsed"]), world - 1.0)
+    # per-rank scalars gathered in rank order (bench's rank_ms_per_step)
+    assert d["per_rank"].tolist() == [10.0 * r + 0.5 for r in range(world)]
     assert float(d["solved"]) == total
     b = bench.make_global_batch("config3", total)
     full = cpu_solver.cpu_solve(mo.default_params(b.horizon), b.x0, b.ref, b.u_prev, nthreads=2)

@@ -206,3 +206,52 @@ def test_served_unpolished_and_nan_against_launch(cuda, monkeypatch, capped):
         assert sa == sb and np.array_equal(ia, ib), q
         if sa in (_lib.SOLVED, _lib.SOLVED_INACCURATE, _lib.MAX_ITER_REACHED):
             assert np.array_equal(Ua, Ub), q
+
+
+def test_two_threads_on_two_workspaces(cuda, monkeypatch):
+    """Two threads, each running its own closed-loop-like sequence of B = 1 requests on its own
+    workspace of the same device at the same time: every answer equals the batch launch's bit for bit.
+    A request stops the other workspace's wave only while that workspace is between calls (its lock
+    is free), so no pending request is overwritten and no call runs into the 30 s timeout."""
+    import threading
+
+    from mpcqp import scenarios
+    from mpcqp.config import MPCConfig
+    from mpcqp.control.mpc_controller import BatchedMPCController
+
+    monkeypatch.setenv("MPCQP_B1_SERVER", "1")
+    N, Q = 10, 60
+    b = scenarios.config3(Q, horizon=N, seed=23)
+    params = MPCConfig(horizon=N).to_parameters(0.8)
+    ref_c = BatchedMPCController(params, Q, device="cuda:0")
+    sol = ref_c.solve_batch(b.x0, b.ref, b.u_prev)
+    exp_st, exp_U = sol.status.cpu().numpy().copy(), sol.U.cpu().numpy().copy()
+    ref_c.close()
+    ctrls = [BatchedMPCController(params, 1, device="cuda:0") for _ in range(2)]
+    results = [[], []]
+    errors = []
+
+    def run(t):
+        try:
+            for rep in range(3):
+                for q in range(t, Q, 2) if rep % 2 == 0 else range(Q - 1 - t, -1, -2):
+                    st, u0, X, U = ctrls[t].solve_one(b.x0[q], b.ref[q], b.u_prev[q])
+                    results[t].append((q, st, U.copy()))
+        except Exception as exc:  # pragma: no cover - reported below
+            errors.append(repr(exc))
+
+    th = [threading.Thread(target=run, args=(t,)) for t in range(2)]
+    t0 = time.perf_counter()
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=60)
+    assert not any(t.is_alive() for t in th), "a served call hung"
+    assert not errors, errors
+    assert time.perf_counter() - t0 < 20.0
+    for t in range(2):
+        assert len(results[t]) == 3 * (Q // 2)
+        for q, st, U in results[t]:
+            assert st == exp_st[q] == 1 and np.array_equal(U, exp_U[q]), (t, q)
+    for c in ctrls:
+        c.close()
