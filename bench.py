@@ -678,10 +678,12 @@ OSQP_SETTINGS = {"scaling": 10, "polish_from": 0, "polish_near": 0.0}
 
 
 def osqp_settings_leg(params, x0, ref, u_prev, steps: int, warmup: int, device, method: str, extra: dict,
-                      check: int) -> dict:
+                      check: int) -> Callable[[], dict]:
     """The same batch with OSQP's own defaults where this build's differ (10 Ruiz passes, one polish
     after ADMM stops; mpc_controller.py:119-132 sets nothing else), timed like the headline leg
-    (events on the launch stream around each step's solve launch), spot-checked the same way."""
+    (events on the launch stream around each step's solve launch), spot-checked the same way.
+    Runs its GPU part now and returns the function that builds its record (host copies and the
+    spot check), so the caller can run its GPU legs back to back and check afterwards."""
     import torch
 
     from mpcqp import _lib
@@ -708,41 +710,56 @@ def osqp_settings_leg(params, x0, ref, u_prev, steps: int, warmup: int, device, 
                 ev[k][1].record(stream)
 
         elapsed = timed_steps(step, steps, warmup, DistContext(), lambda: torch.cuda.synchronize(device))
-        k2_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in ev]))
-        status = ctrl._status[:B].cpu().numpy()
-        iters = ctrl._iters[:B].cpu().numpy()
-        flops = qp_flops(N, iters, scaling=int(ctrl._cparams.scaling), check=int(ctrl._cparams.check_termination))
-        tf = float(flops.sum()) / (k2_ms * 1e-3) / 1e12
-        out = {
-            "value": float((status == 1).sum()) * steps / elapsed,
-            "unit": "QP/s",
-            "ms_per_step": 1e3 * elapsed / steps,
-            "k_solve_ms": k2_ms,
-            "method": method_label(ctrl._cparams),
-            "solver_settings": solver_settings(ctrl._cparams),
-            "solved_fraction": float((status == 1).mean()),
-            "iters_mean": {"admm": float(iters[:, 0].mean()), "polish": float(iters[:, 1].mean())},
-            "roofline": {"bound": "fp64_valu", "achieved": tf, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
-                         "frac": tf / FP64_PEAK_TFLOPS},
-            "note": "the headline batch under OSQP's defaults where this build's defaults differ (scaling 10, "
-                    "polish once after ADMM); same timing rule as the headline line",
-        }
-        if check > 0:
-            idx = np.unique(np.linspace(0, B - 1, min(B, check)).astype(int))
-            out["rel_err"] = spot_check(params, x0, ref, u_prev, ctrl._U[:B].cpu().numpy(),
-                                        ctrl._active[:B].cpu().numpy(), status, idx, iters, settings=sett)
-        return out
-    finally:
+    except BaseException:
         ctrl.close()
+        raise
+
+    def finish() -> dict:
+        try:
+            return _osqp_record(ctrl, ev, elapsed, steps, params, x0, ref, u_prev, check, sett)
+        finally:
+            ctrl.close()
+
+    return finish
 
 
-def pipelined_leg(params, x0, ref, u_prev, steps: int, warmup: int, device, method: str, extra: dict,
-                  U_ref, streams: int = 2) -> dict:
+def _osqp_record(ctrl, ev, elapsed, steps, params, x0, ref, u_prev, check, sett) -> dict:
+    B, N = len(x0), int(params.horizon)
+    k2_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in ev]))
+    status = ctrl._status[:B].cpu().numpy()
+    iters = ctrl._iters[:B].cpu().numpy()
+    flops = qp_flops(N, iters, scaling=int(ctrl._cparams.scaling), check=int(ctrl._cparams.check_termination))
+    tf = float(flops.sum()) / (k2_ms * 1e-3) / 1e12
+    out = {
+        "value": float((status == 1).sum()) * steps / elapsed,
+        "unit": "QP/s",
+        "ms_per_step": 1e3 * elapsed / steps,
+        "k_solve_ms": k2_ms,
+        "method": method_label(ctrl._cparams),
+        "solver_settings": solver_settings(ctrl._cparams),
+        "solved_fraction": float((status == 1).mean()),
+        "iters_mean": {"admm": float(iters[:, 0].mean()), "polish": float(iters[:, 1].mean())},
+        "roofline": {"bound": "fp64_valu", "achieved": tf, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
+                     "frac": tf / FP64_PEAK_TFLOPS},
+        "note": "the headline batch under OSQP's defaults where this build's defaults differ (scaling 10, "
+                "polish once after ADMM); same timing rule as the headline line; run before the headline "
+                "(its GPU part), checked after it",
+    }
+    if check > 0:
+        idx = np.unique(np.linspace(0, B - 1, min(B, check)).astype(int))
+        out["rel_err"] = spot_check(params, x0, ref, u_prev, ctrl._U[:B].cpu().numpy(),
+                                    ctrl._active[:B].cpu().numpy(), status, idx, iters, settings=sett)
+    return out
+
+
+def pipelined_leg(params, x0, ref, u_prev, steps: int, warmup: int, device, method: str,
+                  extra: dict, streams: int = 2) -> Callable[[object], dict]:
     """The headline batch solved `steps` times with step k on stream k % `streams` (each stream its own
     workspace and outputs), so one batch's dispatch tail -- its slowest QPs, DESIGN.md §5 -- overlaps
     the next batch's start.  Reported beside `value`, never as it: every step is still one whole batch
     with its own build and solve, but `streams` batches may be in flight (a serving front end with
-    independent requests; a closed loop whose next batch needs this one's u0 cannot do this)."""
+    independent requests; a closed loop whose next batch needs this one's u0 cannot do this).  Runs
+    its GPU part now; the returned function takes the headline's U and builds the record."""
     import torch
 
     from mpcqp import _lib
@@ -771,22 +788,31 @@ def pipelined_leg(params, x0, ref, u_prev, steps: int, warmup: int, device, meth
 
         elapsed = timed_steps(step, steps, max(warmup, streams), DistContext(),
                               lambda: torch.cuda.synchronize(device))
-        solved = float((ctrls[0]._status[:B] == 1).sum().item())
-        same = all(torch.equal(c._U[:B], U_ref) for c in ctrls)
-        return {
-            "value": solved * steps / elapsed,
-            "unit": "QP/s",
-            "streams": streams,
-            "ms_per_step": 1e3 * elapsed / steps,
-            "identical_to_headline": bool(same),
-            "note": f"the headline batch, step k on stream k % {streams}: consecutive batches overlap, so one "
-                    "batch's slowest QPs share the GPU with the next batch's start; same timing rule as "
-                    "the headline line (K steps between synchronizations); not the headline value, "
-                    "which runs one batch at a time",
-        }
-    finally:
+    except BaseException:
         for c in ctrls:
             c.close()
+        raise
+
+    def finish(U_ref) -> dict:
+        try:
+            solved = float((ctrls[0]._status[:B] == 1).sum().item())
+            same = all(torch.equal(c._U[:B], U_ref) for c in ctrls)
+            return {
+                "value": solved * steps / elapsed,
+                "unit": "QP/s",
+                "streams": streams,
+                "ms_per_step": 1e3 * elapsed / steps,
+                "identical_to_headline": bool(same),
+                "note": f"the headline batch, step k on stream k % {streams}: consecutive batches overlap, so one "
+                        "batch's slowest QPs share the GPU with the next batch's start; same timing rule as "
+                        "the headline line (K steps between synchronizations); not the headline value, "
+                        "which runs one batch at a time; run before the headline, compared with it after",
+            }
+        finally:
+            for c in ctrls:
+                c.close()
+
+    return finish
 
 
 def strong_leg(ctx: DistContext, steps: int, warmup: int, method: str, extra: dict, total: int = 16384,
@@ -955,6 +981,18 @@ def main() -> int:
         if ev is not None:
             ev[2].record(stream)
 
+    # The one-GPU line's secondary legs run their GPU parts first, back to back and straight into the
+    # headline's warmup; their host work (copies, spot checks) waits until after the headline.  They
+    # are ~15 ms of GPU work, about what the MI355X takes to reach its sustained clock from idle
+    # (203 -> 188 us per headline step over its first ~80 launches), so the headline's
+    # K steps run at the clock the GPU holds under load rather than inside the ramp.
+    pre_legs = {}
+    if world == 1 and not args.no_osqp_settings:
+        pre_legs["osqp_settings"] = osqp_settings_leg(params, x0, ref, u_prev, args.steps, args.warmup, device,
+                                                      args.method, extra, min(args.check_sample, 256))
+    if world == 1 and not args.no_pipelined:
+        pre_legs["pipelined"] = pipelined_leg(params, x0, ref, u_prev, args.steps, args.warmup, device,
+                                              args.method, extra)
     elapsed = timed_steps(step, args.steps, args.warmup, ctx, lambda: torch.cuda.synchronize(device))
     timed = events[::args.event_every]
     if fused:
@@ -1076,12 +1114,12 @@ def main() -> int:
         if rank == 0:
             out["config5"] = rec
     if rank == 0:
-        if world == 1 and not args.no_pipelined:
-            out["pipelined"] = pipelined_leg(params, x0, ref, u_prev, args.steps, args.warmup, device, args.method,
-                                             extra, ctrl._U[:B])
-        if world == 1 and not args.no_osqp_settings:
-            out["osqp_settings"] = osqp_settings_leg(params, x0, ref, u_prev, args.steps, args.warmup, device,
-                                                     args.method, extra, min(args.check_sample, 256))
+        if "pipelined" in pre_legs:
+            out["pipelined"] = pre_legs["pipelined"](ctrl._U[:B])
+        if "osqp_settings" in pre_legs:
+            out["osqp_settings"] = pre_legs["osqp_settings"]()
+        out["leg_order"] = (list(pre_legs) + ["headline"] if pre_legs else ["headline"]) + \
+            (["strong_config4"] if headline and not args.no_strong else [])
         if world == 1 and args.cpu_seconds > 0:
             out["cpu_baseline"] = cpu_baseline(params, x0, ref, u_prev, args.cpu_seconds, settings=extra)
         if world == 1 and not args.no_config1:
