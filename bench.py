@@ -816,19 +816,20 @@ def pipelined_leg(params, x0, ref, u_prev, steps: int, warmup: int, device, meth
 
 
 def strong_leg(ctx: DistContext, steps: int, warmup: int, method: str, extra: dict, total: int = 16384,
-               config: str = "config4", check: int = 64) -> Optional[dict]:
+               config: str = "config4", check: int = 64, batch=None) -> Callable[[], Optional[dict]]:
     """BASELINE config 4 as strong scaling: a fixed global batch (16384 Monte-Carlo start poses, N = 30)
     split contiguously over the ranks, timed like the headline (warmup, then `steps` steps between
     barriers + device syncs, MAX over ranks), the per-QP results gathered to rank 0 afterwards and
     spot-checked there.  Every world size runs it, N = 1 included, so the driver's per-N lines carry
-    the strong-scaling curve beside the weak headline.  Returns the record on rank 0."""
+    the strong-scaling curve beside the weak headline.  Runs its GPU part now and returns the function
+    (collective: every rank calls it) that gathers, checks and returns the record on rank 0."""
     import torch
 
     from mpcqp import _lib
     from mpcqp.config import MPCConfig
     from mpcqp.control.mpc_controller import BatchedMPCController
 
-    batch = make_global_batch(config, total)
+    batch = batch if batch is not None else make_global_batch(config, total)
     lo, hi = shard_bounds(total, ctx.world, ctx.rank)
     counts = shard_counts(total, ctx.world)
     B = hi - lo
@@ -847,40 +848,49 @@ def strong_leg(ctx: DistContext, steps: int, warmup: int, method: str, extra: di
                        "solve")
 
         elapsed = timed_steps(step, steps, warmup, ctx, lambda: torch.cuda.synchronize(ctx.device))
-        status = ctrl._status[:B]
-        rank_s = gather_scalar(ctx, elapsed)
-        T, (solved,) = reduce_stats(ctx, elapsed, [float((status == 1).sum().item())])
-        g = {k: gather_rows(ctx, t[:B], counts).cpu().numpy() for k, t in
-             (("status", ctrl._status), ("U", ctrl._U), ("active", ctrl._active))}
-        if ctx.rank != 0:
-            return None
-        out = {
-            "metric": f"MPC QP solves/s (horizon={batch.horizon}, global batch={total}), strong scaling",
-            "workload": batch.name,
-            "value": solved * steps / T,
-            "unit": "QP/s",
-            "n_gpus": ctx.world,
-            "scaling": "strong",
-            "global_batch": total,
-            "batch_per_gpu": counts,
-            "ms_per_step": 1e3 * T / steps,
-            # each rank's own elapsed time per step (the line's ms_per_step is their MAX): shard imbalance
-            "rank_ms_per_step": [1e3 * e / steps for e in rank_s],
-            "steps": steps,
-            "warmup": warmup,
-            "solved_fraction": solved / total,
-            "note": "BASELINE config 4: the fixed global batch split over the ranks, the same timing rule as the "
-                    "headline (barriers + device syncs around the K steps, MAX over ranks); no data-path "
-                    "collective, one gather of the results after timing",
-        }
-        if check > 0:
-            idx = np.unique(np.linspace(0, total - 1, min(total, check)).astype(int))
-            out["rel_err"] = spot_check(params, batch.x0, batch.ref, batch.u_prev, g["U"], g["active"], g["status"],
-                                        idx, settings=extra)
-            out["rel_err"]["gathered_qps"] = int(len(g["status"]))
-        return out
-    finally:
+    except BaseException:
         ctrl.close()
+        raise
+
+    def finish() -> Optional[dict]:
+        try:
+            status = ctrl._status[:B]
+            rank_s = gather_scalar(ctx, elapsed)
+            T, (solved,) = reduce_stats(ctx, elapsed, [float((status == 1).sum().item())])
+            g = {k: gather_rows(ctx, t[:B], counts).cpu().numpy() for k, t in
+                 (("status", ctrl._status), ("U", ctrl._U), ("active", ctrl._active))}
+            if ctx.rank != 0:
+                return None
+            out = {
+                "metric": f"MPC QP solves/s (horizon={batch.horizon}, global batch={total}), strong scaling",
+                "workload": batch.name,
+                "value": solved * steps / T,
+                "unit": "QP/s",
+                "n_gpus": ctx.world,
+                "scaling": "strong",
+                "global_batch": total,
+                "batch_per_gpu": counts,
+                "ms_per_step": 1e3 * T / steps,
+                # each rank's own elapsed time per step (the line's ms_per_step is their MAX): shard imbalance
+                "rank_ms_per_step": [1e3 * e / steps for e in rank_s],
+                "steps": steps,
+                "warmup": warmup,
+                "solved_fraction": solved / total,
+                "note": "BASELINE config 4: the fixed global batch split over the ranks, the same timing rule as the "
+                        "headline (barriers + device syncs around the K steps, MAX over ranks); no data-path "
+                        "collective, one gather of the results after timing; run before the headline (its GPU "
+                        "part), gathered and checked after it",
+            }
+            if check > 0:
+                idx = np.unique(np.linspace(0, total - 1, min(total, check)).astype(int))
+                out["rel_err"] = spot_check(params, batch.x0, batch.ref, batch.u_prev, g["U"], g["active"],
+                                            g["status"], idx, settings=extra)
+                out["rel_err"]["gathered_qps"] = int(len(g["status"]))
+            return out
+        finally:
+            ctrl.close()
+
+    return finish
 
 
 # ------------------------------------------------------------------ main
@@ -981,11 +991,15 @@ def main() -> int:
         if ev is not None:
             ev[2].record(stream)
 
-    # The one-GPU line's secondary legs run their GPU parts first, back to back and straight into the
-    # headline's warmup; their host work (copies, spot checks) waits until after the headline.  They
-    # are ~15 ms of GPU work, about what the MI355X takes to reach its sustained clock from idle
-    # (203 -> 188 us per headline step over its first ~80 launches), so the headline's
-    # K steps run at the clock the GPU holds under load rather than inside the ramp.
+    # The secondary legs (OSQP settings and pipelined on one GPU; config 4 strong scaling at every world
+    # size) run their GPU parts first, back to back and straight into the headline's warmup; their host
+    # work (copies, gathers, spot checks) waits until after the headline.  Together they are ~35 ms of
+    # GPU work, more than the MI355X takes to reach its sustained clock from idle (a step
+    # takes 203 -> 188 us over its first ~80 launches; 20 steps after 5 warm ones read 8 % low,
+    # profiles/r06/warmup_matrix.txt), so the headline's K steps run at the clock the GPU holds under
+    # load rather than inside its ramp.  The line records the order (leg_order).
+    headline = args.config == "config3" and not args.horizon and not strong
+    strong_batch = make_global_batch("config4", 16384) if headline and not args.no_strong else None
     pre_legs = {}
     if world == 1 and not args.no_osqp_settings:
         pre_legs["osqp_settings"] = osqp_settings_leg(params, x0, ref, u_prev, args.steps, args.warmup, device,
@@ -993,6 +1007,8 @@ def main() -> int:
     if world == 1 and not args.no_pipelined:
         pre_legs["pipelined"] = pipelined_leg(params, x0, ref, u_prev, args.steps, args.warmup, device,
                                               args.method, extra)
+    if strong_batch is not None:  # every rank (collectives in its record step, after the headline)
+        pre_legs["strong_config4"] = strong_leg(ctx, args.steps, args.warmup, args.method, extra, batch=strong_batch)
     elapsed = timed_steps(step, args.steps, args.warmup, ctx, lambda: torch.cuda.synchronize(device))
     timed = events[::args.event_every]
     if fused:
@@ -1102,11 +1118,10 @@ def main() -> int:
                                         g["status"], idx, g["iters"], settings=extra)
             out["rel_err"]["gathered_qps"] = int(len(g["status"]))
             out["rel_err"]["gathered_solved"] = int((g["status"] == 1).sum())
-    # legs every rank takes part in (collectives inside): config 4 as strong scaling at every world size,
-    # config 5 sharded by vehicle past one GPU
-    headline = args.config == "config3" and not args.horizon and not strong
-    if headline and not args.no_strong:
-        rec = strong_leg(ctx, args.steps, args.warmup, args.method, extra)
+    # legs every rank takes part in (collectives inside): config 4 as strong scaling at every world size
+    # (its GPU part ran before the headline), config 5 sharded by vehicle past one GPU
+    if "strong_config4" in pre_legs:
+        rec = pre_legs["strong_config4"]()
         if rank == 0:
             out["strong_config4"] = rec
     if headline and world > 1 and not args.no_config5:
@@ -1118,8 +1133,7 @@ def main() -> int:
             out["pipelined"] = pre_legs["pipelined"](ctrl._U[:B])
         if "osqp_settings" in pre_legs:
             out["osqp_settings"] = pre_legs["osqp_settings"]()
-        out["leg_order"] = (list(pre_legs) + ["headline"] if pre_legs else ["headline"]) + \
-            (["strong_config4"] if headline and not args.no_strong else [])
+        out["leg_order"] = list(pre_legs) + ["headline"]
         if world == 1 and args.cpu_seconds > 0:
             out["cpu_baseline"] = cpu_baseline(params, x0, ref, u_prev, args.cpu_seconds, settings=extra)
         if world == 1 and not args.no_config1:
