@@ -141,6 +141,19 @@ struct Mid {
 
   __device__ __forceinline__ static void sync() { __syncthreads(); }
 
+  // The CW values v[h CW + c] (c < CW) of an LDS vector, in every lane for the fmac_bc products: lane
+  // l loads element h CW + l (one conflict-free per-lane read) and the permlane broadcast (bcast,
+  // mpcqp_common.h) replicates each 16-lane row into all four, so a dense product reads its operand
+  // through DPP row_newbcast.  A broadcast LDS read per column instead (the same address in every lane,
+  // 512 B out of the LDS per read) kept the LDS output port busy: 8 waves per CU x CW reads per product
+  // or pivot is ~1.3k cycles at N = 40, the measured cost of a sweep step and of an ADMM iteration's
+  // product (round 5: 1.5k / 2.25k cycles).  Every lane of the wave must call this.
+  static constexpr int kNWc = (CW + 15) / 16;
+  __device__ __forceinline__ void lbcast(const double* v, double w[4]) const {
+    const double x = lane < CW ? v[h * CW + lane] : 0.0;
+    bcast<kNWc>(x, w);
+  }
+
   // opaque per-lane data at the top of solver iterations (keeps LICM from hoisting derived values)
   __device__ __forceinline__ void opaque() {
     asm volatile("" : "+v"(i));
@@ -219,9 +232,13 @@ struct Mid {
   __device__ __forceinline__ double kmul(double v) {
     if (V) sm->vb[i] = act ? v : 0.0;
     sync();
-    const double* b = sm->vb + h * CW;
+    double w[4];
+    lbcast(sm->vb, w);
     double a[4] = {0.0, 0.0, 0.0, 0.0};
-    piped<CW>([&](auto c) { return b[c]; }, [&](auto c, double bc) { a[c % 4] = fma(r[c], bc, a[c % 4]); });
+    Unroll<0, CW>::run([&](auto cc) {
+      constexpr int c = decltype(cc)::value;
+      fmac_bc<c % 16>(a[c % 4], w[c / 16], r[c]);  // fma(vb[h CW + c], r[c], a): the same bits as fma(r, vb, a)
+    });
     return combine((a[0] + a[1]) + (a[2] + a[3]));
   }
   // the parts' partial sums of row i added on the V thread: s0 + s1, or (s0 + s1) + (s2 + s3)
@@ -241,13 +258,17 @@ struct Mid {
   __device__ __forceinline__ double Pmul(double v) {
     if (V) sm->vb[i] = act ? v : 0.0;
     sync();
-    const double* b = sm->vb + h * CW;
+    double w[4];
+    lbcast(sm->vb, w);
     int ii = i;  // opaque: the column addresses are recomputed per call, not hoisted out of the solver loops
     asm volatile("" : "+v"(ii));
     const double* pc = Pg + (size_t)(h * CW) * kMidLD + ii;
     double a[4] = {0.0, 0.0, 0.0, 0.0};
     piped<CW>([&](auto c) { return pc[(size_t)c * kMidLD]; },
-              [&](auto c, double pv) { a[c % 4] = fma(pv, b[c], a[c % 4]); });
+              [&](auto cc, double pv) {
+                constexpr int c = decltype(cc)::value;
+                fmac_bc<c % 16>(a[c % 4], w[c / 16], pv);
+              });
     return combine((a[0] + a[1]) + (a[2] + a[3]));
   }
 
@@ -329,7 +350,8 @@ struct Mid {
           const double* col = sm->cb[ck & 1];
           const double d = col[k];
           const double aik = col[i];
-          const double* bj = col + h * CW;
+          double w[4];  // the pivot row A[k][j] = A[j][k] of this part's columns, by DPP broadcast
+          lbcast(col, w);
           ok = ok && (d > 0.0) && isfinite(d);
           double inv = __builtin_amdgcn_rcp(d);
           inv = fma(inv, fma(-d, inv, 1.0), inv);
@@ -338,25 +360,26 @@ struct Mid {
           const double cki = aik * inv;
           const double coef = piv ? inv - 1.0 : -cki;
           // the next pivot's column first, published for the next step
+          // fmac_bc: fma(A[k][j], coef, r) -- the same bits as fma(coef, A[k][j], r)
           if constexpr (ck + 1 < CW) {
             if (h == hk) {
-              r[ck + 1] = fma(coef, bj[ck + 1], r[ck + 1]);
+              fmac_bc<(ck + 1) % 16>(r[ck + 1], w[(ck + 1) / 16], coef);
               sm->cb[(ck + 1) & 1][i] = r[ck + 1];
             }
           } else {
             if (h == hk + 1) {
-              r[0] = fma(coef, bj[0], r[0]);
+              fmac_bc<0>(r[0], w[0], coef);
               sm->cb[0][i] = r[0];
             }
           }
-          piped<CW>([&](auto c) { return bj[c]; }, [&](auto jc, double bc) {
+          Unroll<0, CW>::run([&](auto jc) {
             constexpr int c = decltype(jc)::value;
             if constexpr (c == ck + 1) {  // (ck + 1 < CW) done above in the pivot's part
-              if (h != hk) r[c] = fma(coef, bc, r[c]);
+              if (h != hk) fmac_bc<c % 16>(r[c], w[c / 16], coef);
             } else if constexpr (c == 0 && ck + 1 == CW) {  // done above in the next part
-              if (h != hk + 1) r[c] = fma(coef, bc, r[c]);
+              if (h != hk + 1) fmac_bc<c % 16>(r[c], w[c / 16], coef);
             } else {
-              r[c] = fma(coef, bc, r[c]);
+              fmac_bc<c % 16>(r[c], w[c / 16], coef);
             }
           });
           if (h == hk) r[ck] = piv ? -inv : cki;
@@ -403,8 +426,12 @@ struct Mid {
     const double den = 1.0 + delta * cu;
     if (!(den > kRank1Min) || !isfinite(den)) return false;  // uniform
     const double m = (delta / den) * ui;
-    const double* bj = U + h * CW;
-    piped<CW>([&](auto c) { return bj[c]; }, [&](auto c, double bc) { r[c] = fma(bc, m, r[c]); });
+    double w[4];
+    lbcast(U, w);
+    Unroll<0, CW>::run([&](auto cc) {
+      constexpr int c = decltype(cc)::value;
+      fmac_bc<c % 16>(r[c], w[c / 16], m);
+    });
     return true;
   }
   static constexpr int X_() { return S::kNX; }

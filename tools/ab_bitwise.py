@@ -25,6 +25,16 @@ CASES = [  # (config, horizon, batch, pairing, settings)
     ("config3", 10, 1024, "off", {"polish_from": 25}),
     ("config3", 20, 1024, "auto", {"max_iter": 40, "polish": 0}),
 ]
+MID_CASES = [  # the mid-horizon kernel (N = 33..64)
+    ("config3", 33, 1024, "auto", {}),
+    ("config3", 40, 1024, "auto", {}),
+    ("config3", 48, 512, "auto", {}),
+    ("config3", 56, 512, "auto", {}),
+    ("config3", 64, 512, "auto", {}),
+    ("config3", 40, 512, "auto", {"max_iter": 40, "polish": 0}),
+]
+if os.environ.get("MPCQP_AB_MID") == "1":
+    CASES = MID_CASES
 
 
 def child(out: str) -> None:
@@ -50,7 +60,10 @@ def main() -> None:
     ap.add_argument("--libs", nargs=2, required=True)
     ap.add_argument("--out", required=True)
     ap.add_argument("--child", default=None)
+    ap.add_argument("--mid", action="store_true", help="the mid-horizon cases (N = 33..64) instead")
     a = ap.parse_args()
+    if a.mid:
+        os.environ["MPCQP_AB_MID"] = "1"
     if a.child:
         child(a.child)
         return
