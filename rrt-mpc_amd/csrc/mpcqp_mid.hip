@@ -96,7 +96,7 @@ struct MidLds {
   static constexpr int X = S::kNX;
   double vb[X];                 // dense product operand
   double pp[S::kParts - 1][X];  // dense product partial sums of the parts h >= 1
-  double cb[2][X];              // sweep pivot columns (double buffered)
+  double cbb[2][X][2];          // sweep: the pivot pair's two columns per row (double buffered; Mid::sweep)
   double ex[2][5][X + 8];       // neighbour exchange: row i at [i + 4]; 4 zeros either side
   double vec[X];                // per-row broadcast (Ruiz scalings, rank-1 vector)
   double tr[S::kParts][3][X];   // rank-1 terms per part
@@ -332,57 +332,102 @@ struct Mid {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
 
-  // Symmetric sweep on the rows in r[]: afterwards A^{-1} = -r.  Pivot k's column is published by
-  // the half that holds it (LDS, double buffered) and read by every thread: its own A[i][k], the
-  // pivot d = A[k][k] and A[k][j] = A[j][k] of its half's columns.  The next pivot's column is
-  // updated first and published before the rest of the step.  Pivots past n are skipped (their
-  // rows and columns are zero).  false on a non-positive pivot.
+  // Symmetric sweep on the rows in r[], pivots in pairs K = {k, k + 1} (n is even): afterwards A^{-1} = -r.
+  // Sweeping a pair at once is the composition of its two single sweeps: with G = -A_KK^{-1} (2 x 2),
+  //   A[i][j] -> A[i][j] + g_i . A[K][j]   (j not in K),  g_i = A'[i][K] . G,
+  //   A[i][K] -> -g_i - e_i                 (the pair's columns),
+  // where A'[i][K] is A[i][K] minus the unit vector of i when row i is one of the pair (then g_i = -G[i] -
+  // e_i: row i becomes A_KK^{-1} A[K][j], its K entries -A_KK^{-1}[i]).  The part holding the pair's
+  // columns publishes A'[.][K] through LDS (double buffered, row-major pairs); every thread reads its own
+  // A'[i][K], the 2 x 2 block (unit vectors added back), and the two pivot rows A[K][j] = A'[j][K] of its
+  // part's columns by per-lane reads and the DPP broadcast (lbcast).  G comes from the 2 x 2 block's own
+  // sweep in every thread; its pivots are the sequential sweep's (the same non-positive-pivot test).
+  // One barrier per two pivots.  The rounding differs from the pivot-by-pivot sweep; the optimum,
+  // statuses and active sets do not.
+  static constexpr int kSB = 2;
+  static_assert(CW % kSB == 0, "a pivot pair lies inside one column part");
+  // publish A'[i][k0], A'[i][k0 + 1] of this thread's row from its registers c0, c0 + 1
+  template <int C0>
+  __device__ __forceinline__ void publish(double (*q)[kSB], int k0) {
+    double* o = q[i];
+#pragma unroll
+    for (int t = 0; t < kSB; ++t) o[t] = i == k0 + t ? r[C0 + t] - 1.0 : r[C0 + t];
+  }
   __device__ __forceinline__ bool sweep() {
     bool ok = true;
-    // publish pivot 0
-    if (h == 0) sm->cb[0][i] = r[0];
+    if (h == 0) publish<0>(sm->cbb[0], 0);
     for (int hk = 0; hk < kP; ++hk) {
-      Unroll<0, CW>::run([&](auto cc) {
-        constexpr int ck = decltype(cc)::value;
-        const int k = hk * CW + ck;
-        if (k < n) {
+      Unroll<0, CW / kSB>::run([&](auto cbc) {
+        constexpr int cb = decltype(cbc)::value;
+        constexpr int c0 = cb * kSB;  // the pair's first column, local to part hk
+        const int k0 = hk * CW + c0;  // ... and global
+        if (k0 < n) {
           sync();
-          const double* col = sm->cb[ck & 1];
-          const double d = col[k];
-          const double aik = col[i];
-          double w[4];  // the pivot row A[k][j] = A[j][k] of this part's columns, by DPP broadcast
-          lbcast(col, w);
-          ok = ok && (d > 0.0) && isfinite(d);
-          double inv = __builtin_amdgcn_rcp(d);
-          inv = fma(inv, fma(-d, inv, 1.0), inv);
-          inv = fma(inv, fma(-d, inv, 1.0), inv);
-          const bool piv = i == k;
-          const double cki = aik * inv;
-          const double coef = piv ? inv - 1.0 : -cki;
-          // the next pivot's column first, published for the next step
-          // fmac_bc: fma(A[k][j], coef, r) -- the same bits as fma(coef, A[k][j], r)
-          if constexpr (ck + 1 < CW) {
-            if (h == hk) {
-              fmac_bc<(ck + 1) % 16>(r[ck + 1], w[(ck + 1) / 16], coef);
-              sm->cb[(ck + 1) & 1][i] = r[ck + 1];
-            }
-          } else {
-            if (h == hk + 1) {
-              fmac_bc<0>(r[0], w[0], coef);
-              sm->cb[0][i] = r[0];
-            }
+          const int gb = hk * (CW / kSB) + cb;
+          double (*q)[kSB] = sm->cbb[gb & 1];
+          // G = -A_KK^{-1} by the 2 x 2 block's sweep
+          double g00 = q[k0][0] + 1.0, g01 = q[k0][1], g11 = q[k0 + 1][1] + 1.0;
+          ok = ok && (g00 > 0.0) && isfinite(g00);
+          double inv = __builtin_amdgcn_rcp(g00);
+          inv = fma(inv, fma(-g00, inv, 1.0), inv);
+          inv = fma(inv, fma(-g00, inv, 1.0), inv);
+          const double c1 = g01 * inv;
+          g11 = fma(-c1, g01, g11);
+          g00 = -inv;
+          g01 = c1;
+          ok = ok && (g11 > 0.0) && isfinite(g11);
+          double inv1 = __builtin_amdgcn_rcp(g11);
+          inv1 = fma(inv1, fma(-g11, inv1, 1.0), inv1);
+          inv1 = fma(inv1, fma(-g11, inv1, 1.0), inv1);
+          const double c0v = g01 * inv1;
+          g00 = fma(-c0v, g01, g00);
+          g01 = c0v;
+          g11 = -inv1;
+          // g_i = A'[i][K] . G
+          const double a0 = q[i][0], a1 = q[i][1];
+          double gm[kSB];
+          gm[0] = fma(a1, g01, a0 * g00);
+          gm[1] = fma(a1, g11, a0 * g01);
+          // the two pivot rows of this part's columns, by DPP broadcast
+          double w0[4], w1[4];
+          {
+            const double* qp = &q[h * CW][0];
+            const double x0 = lane < CW ? qp[kSB * lane] : 0.0;
+            const double x1 = lane < CW ? qp[kSB * lane + 1] : 0.0;
+            bcast<kNWc>(x0, w0);
+            bcast<kNWc>(x1, w1);
           }
-          Unroll<0, CW>::run([&](auto jc) {
-            constexpr int c = decltype(jc)::value;
-            if constexpr (c == ck + 1) {  // (ck + 1 < CW) done above in the pivot's part
-              if (h != hk) fmac_bc<c % 16>(r[c], w[c / 16], coef);
-            } else if constexpr (c == 0 && ck + 1 == CW) {  // done above in the next part
-              if (h != hk + 1) fmac_bc<c % 16>(r[c], w[c / 16], coef);
-            } else {
-              fmac_bc<c % 16>(r[c], w[c / 16], coef);
-            }
+          __builtin_amdgcn_sched_barrier(0);
+          // fmac_bc: fma(A[K][j], g, r)
+          auto upd = [&](auto jcc, const double g[kSB]) {
+            constexpr int jc = decltype(jcc)::value;
+            fmac_bc<jc % 16>(r[jc], w0[jc / 16], g[0]);
+            fmac_bc<jc % 16>(r[jc], w1[jc / 16], g[1]);
+          };
+          // the next pair's columns first (the part that holds them), published for the next step
+          constexpr int nc0 = c0 + kSB < CW ? c0 + kSB : 0;  // their first register
+          const bool early = (c0 + kSB < CW ? h == hk : h == hk + 1) && k0 + kSB < n;
+          if (early) {
+            upd(std::integral_constant<int, nc0>{}, gm);
+            upd(std::integral_constant<int, nc0 + 1>{}, gm);
+            publish<nc0>(sm->cbb[(gb + 1) & 1], k0 + kSB);
+          }
+          // every other column of this part; no per-column branches (they cost the row's registers:
+          // scratch): the columns done above take a zero update, the pair's own columns are overwritten
+          double gs[kSB];
+#pragma unroll
+          for (int t = 0; t < kSB; ++t) gs[t] = early ? 0.0 : gm[t];
+          Unroll<0, CW>::run([&](auto jcc) {
+            constexpr int jc = decltype(jcc)::value;
+            if constexpr (jc >= nc0 && jc < nc0 + kSB)
+              upd(jcc, gs);
+            else
+              upd(jcc, gm);
           });
-          if (h == hk) r[ck] = piv ? -inv : cki;
+          if (h == hk) {
+#pragma unroll
+            for (int t = 0; t < kSB; ++t) r[c0 + t] = -gm[t] - (i == k0 + t ? 1.0 : 0.0);
+          }
         }
       });
     }
