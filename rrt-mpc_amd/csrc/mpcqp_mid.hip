@@ -98,7 +98,9 @@ struct MidLds {
   double pp[S::kParts - 1][X];  // dense product partial sums of the parts h >= 1
   double cbb[2][X][2];          // sweep: the pivot pair's two columns per row (double buffered; Mid::sweep)
   double ex[2][5][X + 8];       // neighbour exchange: row i at [i + 4]; 4 zeros either side
-  double vec[X];                // per-row broadcast (Ruiz scalings, rank-1 vector)
+  double vec[X];                // per-row broadcast (Ruiz scalings, rank-1 vector; ADMM step: C' tmp's own terms)
+  double abx[2][X + 4];         // ADMM step: the terms of C' tmp for the variables 2 / 4 back (4 zeros past X)
+  double qq[X];                 // ADMM step: q per row
   double tr[S::kParts][3][X];   // rank-1 terms per part
   double band[5][X];            // form(): band entries (i, i - 4 .. i + 4) per row
   double cf[6][X];              // Cbar coefficients per variable (rank-1 rows)
@@ -254,6 +256,63 @@ struct Mid {
     return V && act ? s : 0.0;
   }
   __device__ __forceinline__ double inv_mul(double v) { return -kmul(v); }
+
+  // The linear part of an ADMM iteration with two barriers instead of four, bit for bit the operations
+  // of rhs = CTmul(tmp) + sg x - qv, xa = alpha inv_mul(rhs), Cmul(xa) (which cross the parts and row
+  // waves through an exchange, the operand and the partial sums: one barrier each):
+  //   1. each row's own terms of C' tmp and its x go to LDS;
+  //   2. lane l assembles rhs of its part's column h CW + l from them (the terms 2 and 4 rows ahead
+  //      read directly), broadcasts it by DPP into the product, and every part's partial sum goes to LDS;
+  //   3. the V threads add the parts' sums of their row AND of the rows 2 and 4 back (the same sums in
+  //      the same order as the owners'), which is all Cbar xa needs.
+  // xa and za (= Cbar xa) on V threads.
+  __device__ __forceinline__ void admm_linear(const double tmp[3], double sg, double x, double alpha, double& xa,
+                                              double za[3]) {
+    if (V) {
+      sm->abx[0][i] = c11 * tmp[1] + c21 * tmp[2];  // to the variable 2 back
+      sm->abx[1][i] = c22 * tmp[2];                 // to the variable 4 back
+      sm->vec[i] = (c0 * tmp[0] + c10 * tmp[1]) + c20 * tmp[2];
+      sm->vb[i] = x;
+    }
+    sync();
+    double rj = 0.0;
+    if (lane < CW) {
+      const int j = h * CW + lane;
+      const double ct = sm->vec[j] + (sm->abx[0][j + 2] + sm->abx[1][j + 4]);  // CTmul's t + (p2 + p4)
+      const double v = ct + sg * sm->vb[j] - sm->qq[j];
+      rj = j < n ? v : 0.0;
+    }
+    double w[4];
+    bcast<kNWc>(rj, w);
+    double a[4] = {0.0, 0.0, 0.0, 0.0};
+    Unroll<0, CW>::run([&](auto cc) {
+      constexpr int c = decltype(cc)::value;
+      fmac_bc<c % 16>(a[c % 4], w[c / 16], r[c]);
+    });
+    sm->tr[h][0][i] = (a[0] + a[1]) + (a[2] + a[3]);
+    sync();
+    if (V) {
+      auto xa_of = [&](int row) -> double {  // combine's sum, inv_mul's sign, alpha
+        const double* q0 = &sm->tr[0][0][0];
+        constexpr int st = 3 * S::kNX;  // stride between the parts' rows of tr
+        double s;
+        if constexpr (kP == 2)
+          s = q0[row] + q0[st + row];
+        else
+          s = (q0[row] + q0[st + row]) + (q0[2 * st + row] + q0[3 * st + row]);
+        return alpha * -(row < n ? s : 0.0);
+      };
+      xa = xa_of(i);
+      const double xm2 = i >= 2 ? xa_of(i - 2) : 0.0;
+      const double xm4 = i >= 4 ? xa_of(i - 4) : 0.0;
+      za[0] = c0 * xa;
+      za[1] = c10 * xa + c11 * xm2;
+      za[2] = (c20 * xa + c21 * xm2) + c22 * xm4;
+    } else {
+      xa = 0.0;
+      za[0] = za[1] = za[2] = 0.0;
+    }
+  }
   // (Pbar v)_i from the workspace copy (coalesced: lanes read consecutive rows of one column)
   __device__ __forceinline__ double Pmul(double v) {
     if (V) sm->vb[i] = act ? v : 0.0;
@@ -983,6 +1042,7 @@ __device__ __forceinline__ int mid_admm(const mpcqp_params& p, Mid<NT>& C, MidAd
   const bool early = p.polish != 0 && p.polish_from > 0;
   int ev = kMidMaxIter;
   bool done = false;
+  if (C.V) C.sm->qq[C.i] = C.qv;  // read after the first iteration's barrier
   while (S.it < p.max_iter && !done) {
     if (S.need_fact) {
       const double rw[3] = {S.rho, S.rho, S.rho};
@@ -1012,10 +1072,8 @@ __device__ __forceinline__ int mid_admm(const mpcqp_params& p, Mid<NT>& C, MidAd
       double tmp[3];
 #pragma unroll
       for (int k = 0; k < 3; ++k) tmp[k] = rho * S.z[k] - S.y[k];
-      const double rhs = C.CTmul(tmp) + sg * S.x - C.qv;
-      const double xa = alpha * C.inv_mul(rhs);
-      double za[3];
-      C.Cmul(xa, za);
+      double xa, za[3];
+      C.admm_linear(tmp, sg, S.x, alpha, xa, za);
       S.x = xa + oma * S.x;
 #pragma unroll
       for (int k = 0; k < 3; ++k) {
@@ -1256,6 +1314,7 @@ __global__ __launch_bounds__(MidShape<NT>::kThreads, kMidWaves) void k_solve_mid
     const int slot = e / 40, q = (e / 8) % 5, k = e % 8;
     sm.ex[slot][q][k < 4 ? k : S::kNX + k] = 0.0;
   }
+  if (tid < 8) sm.abx[tid >> 2][S::kNX + (tid & 3)] = 0.0;  // read as the rows past the end
   const int N = p.horizon;
   const double* mb = model + (size_t)b * model_stride(N);
   for (int e = tid; e < model_stride(N); e += S::kThreads) sm.model[e] = mb[e];
