@@ -29,13 +29,20 @@ constexpr int kMidLD = 128;  // row stride (doubles) of the workspace Pbar
 #ifdef MPCQP_MID_STAMPS
 __device__ unsigned long long g_mid_stamps[16];
 struct MidStamps {
-  unsigned long long acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  unsigned long long t = 0;
-  __device__ __forceinline__ void begin() { t = __builtin_amdgcn_s_memtime(); }
+  // 0..7 the phases, 9..15 the setup's sub-phases (mark()); g_mid_stamps[8] counts the QPs
+  unsigned long long acc[16] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+  unsigned long long t = 0, t2 = 0;
+  __device__ __forceinline__ void begin() { t = t2 = __builtin_amdgcn_s_memtime(); }
   __device__ __forceinline__ void end(int k) { acc[k] += __builtin_amdgcn_s_memtime() - t; }
+  __device__ __forceinline__ void mark(int k) {
+    const unsigned long long now = __builtin_amdgcn_s_memtime();
+    acc[k] += now - t2;
+    t2 = now;
+  }
   __device__ __forceinline__ void flush() {
     if (threadIdx.x == 0) {
-      for (int k = 0; k < 8; ++k) atomicAdd(&g_mid_stamps[k], acc[k]);
+      for (int k = 0; k < 16; ++k)
+        if (k != 8) atomicAdd(&g_mid_stamps[k], acc[k]);
       atomicAdd(&g_mid_stamps[8], 1ull);
     }
   }
@@ -44,6 +51,7 @@ struct MidStamps {
 struct MidStamps {
   __device__ __forceinline__ void begin() {}
   __device__ __forceinline__ void end(int) {}
+  __device__ __forceinline__ void mark(int) {}
   __device__ __forceinline__ void flush() {}
 };
 #endif
@@ -54,7 +62,8 @@ constexpr int kMidWaves = 2;  // waves per SIMD the register allocation targets
 // the NT doubles of the row (hoisting every load ahead of the FMAs spills the row).
 template <int NT, int G = 4, class Ld, class F>
 __device__ __forceinline__ void piped(Ld&& ld, F&& f) {
-  double cur[G], nxt[G];
+  using T = decltype(ld(std::integral_constant<int, 0>{}));
+  T cur[G], nxt[G];
   Unroll<0, G>::run([&](auto kc) {
     constexpr int k = decltype(kc)::value;
     if constexpr (k < NT) cur[k] = ld(std::integral_constant<int, k>{});
@@ -75,6 +84,10 @@ __device__ __forceinline__ void piped(Ld&& ld, F&& f) {
     Unroll<0, G>::run([&](auto kc) { cur[decltype(kc)::value] = nxt[decltype(kc)::value]; });
   });
 }
+
+struct Rq {  // one step's loads of the prefix / free-response recurrence (mid_setup)
+  double a, c, r;
+};
 
 template <int NT>
 struct MidShape {
@@ -111,7 +124,7 @@ struct MidLds {
   unsigned long long msk[2][3][2];  // changed-row ballots of the row waves (two slots)
   double model[model_stride(NT)];
   double pre[4][NT + 1];
-  double err[NT + 1][4];
+  double err[4][NT + 1];
   double g[S::kNX + 2];
   double W[S::kNX + 2];
 };
@@ -579,31 +592,80 @@ __device__ __forceinline__ bool mid_setup(const mpcqp_params& p, Mid<NT>& C) {
   const double* x0 = mdl + 11 * N + 4;
   const double* up = mdl + 11 * N + 8;
   const int tid = threadIdx.x;
-  if (tid < 4) {  // prefix sums of alpha, beta, gamma, eta
-    const double* a = mdl + tid * N;
-    double acc = 0.0;
-    sm.pre[tid][0] = 0.0;
-    for (int k = 0; k < N; ++k) {
-      acc += a[k];
-      sm.pre[tid][k + 1] = acc;
+  // prefix sums and free response: ONE sequential recurrence on lanes 0..3 of wave 0 (one instruction
+  // stream, every load ahead of the chain; the one-wave kernel's setup): lanes 0 / 1 the prefix sums of
+  // alpha / gamma (pre[0] / pre[2]), lanes 2 / 3 the free response's x / y at W = 0,
+  // acc <- acc + A[k] h + B[k] v_k + C[k], with (h, v, C) = (1, 0, 0) on the prefix lanes (exactly
+  // acc + A[k]) and (psi, v_0 at k = 0, c0 | c1) on the free-response lanes.  The heading and speed rows
+  // of e_m are lane-parallel (wave 1).
+  if (tid < 4) {
+    const bool fr = tid >= 2;
+    const int q = tid & 1;
+    const double* __restrict__ A = mdl + (q ? 2 * N : 0);
+    const double* __restrict__ Bv = mdl + (q ? 3 * N : N);
+    const double* __restrict__ Cc = mdl + (q ? 6 * N : 5 * N);
+    const double* __restrict__ R = rr + 4 + q;
+    const double h = fr ? x0[2] : 1.0, v0 = fr ? x0[3] : 0.0, one = fr ? 1.0 : 0.0;
+    double acc = fr ? x0[q] : 0.0;
+    double* __restrict__ out = fr ? sm.err[q] : sm.pre[2 * q];
+    if (!fr) out[0] = 0.0;
+    const double b0 = Bv[0];
+    // the loads issued a group ahead of the chain (piped): all of them up front is 3 NT registers
+    piped<NT, 8>(
+        [&](auto kc) {
+          constexpr int k = decltype(kc)::value;
+          const int kk = k < N ? k : N - 1;  // (steps past N: loaded in range, not used)
+          return Rq{A[kk], Cc[kk], R[4 * kk]};
+        },
+        [&](auto kc, const Rq& v) {
+          constexpr int k = decltype(kc)::value;
+          if (k < N) {
+            acc = acc + v.a * h + (k == 0 ? b0 : 0.0) * (k == 0 ? v0 : 0.0) + one * v.c;
+            out[k + 1] = acc - one * v.r;
+          }
+        });
+  } else if (tid >= kWave && tid < kWave + N) {
+    const int m = tid - kWave + 1;
+    sm.err[2][m] = x0[2] - rr[4 * m + 2];
+    sm.err[3][m] = 0.0 - rr[4 * m + 3];
+  }
+  // the band table of the input cost: kinds 0 / 1 / 2 (speed, the last speed, steering), the entry for
+  // column col of row i at [kind][kNX + col - i] (one LDS read per column below instead of a compare-and-
+  // select per column and band entry).  It lives in the rank-1 buffer, unused until the polish.
+  const double r00 = 0.5 * (p.r[0] + p.r[0]) / (dt * dt), r10 = 0.5 * (p.r[2] + p.r[1]) / dt;
+  const double r11 = 0.5 * (p.r[3] + p.r[3]);
+  double* bt = &sm.tr[0][0][0];
+  static_assert(sizeof(sm.tr) >= sizeof(double) * 3 * 2 * S::kNX, "band table in the rank-1 buffer");
+  for (int e = tid; e < 3 * 2 * S::kNX; e += S::kThreads) {
+    const int kind = e / (2 * S::kNX), d = e % (2 * S::kNX) - S::kNX;
+    double v = 0.0;
+    if (kind < 2) {
+      if (d == 0) v = kind == 0 ? 2.0 * r00 : r00;
+      if (d == 2 || d == -2) v = -r00;
+      if (d == 1) v = r10;
+      if (d == 3) v = -r10;
+    } else {
+      if (d == 0) v = r11;
+      if (d == -1) v = r10;
+      if (d == -3) v = -r10;
     }
-  } else if (tid == 4) {  // free response at W = 0
-    double px = x0[0], py = x0[1];
-    const double psi = x0[2];
-    for (int m = 1; m <= N; ++m) {
-      const int k = m - 1;
-      const double v = k == 0 ? x0[3] : 0.0;
-      px = px + al[k] * psi + be[k] * v + cz0[k];
-      py = py + ga[k] * psi + et[k] * v + cz1[k];
-      sm.err[m][0] = px - rr[4 * m + 0];
-      sm.err[m][1] = py - rr[4 * m + 1];
-      sm.err[m][2] = psi - rr[4 * m + 2];
-      sm.err[m][3] = 0.0 - rr[4 * m + 3];
-    }
+    bt[e] = v;
   }
   __syncthreads();
+  C.T.mark(9);
 
-  // ---- condense: column `col` of H; rows of this thread's half into r[] (or g for col == n)
+  // ---- condense: column i of H by the backward adjoint recursion, the rows of this thread's part into
+  // r[]; the gradient column (the free response) on a lane of its own, into sm.g.
+  // mu_m = W_m s_m + A_m' mu_{m+1};  H[(k, c'), col] = (B_k e_c')' mu_{k+1}
+  // Every lane runs the same instruction stream (the one-wave kernel's condensing): the gradient column and
+  // the two kinds of variable column differ only in lane constants and in which LDS row a lane reads per
+  // step.  Per step m the column's state sensitivity s = (s0, s1, s2, s3) is
+  //   speed v_{j+1} (i = 2 j):        (be_{j+1}, et_{j+1}, 0, 0) from m = j + 2 on, (0, 0, 0, 1) at m = j + 1
+  //   steering delta_j (i = 2 j + 1): si_j (P_a[m] - P_a[j+1], P_g[m] - P_g[j+1], 1, 0) from m = j + 1 on
+  //   gradient column:                e_m
+  // Part h keeps rows [h CW, h CW + CW), i.e. the steps m = h CW / 2 + 1 .. h CW / 2 + CW / 2, and runs
+  // the recursion only down to its first one.  The gradient lane is row n of part 0 (a padding row),
+  // or, when the rows fill the row waves (n = kNX), a second pass on the last part's first row wave.
   double Q[4][4], QN[4][4];
 #pragma unroll
   for (int a = 0; a < 4; ++a)
@@ -612,102 +674,158 @@ __device__ __forceinline__ bool mid_setup(const mpcqp_params& p, Mid<NT>& C) {
       Q[a][b] = 0.5 * (p.q[4 * a + b] + p.q[4 * b + a]);
       QN[a][b] = 0.5 * (p.q_terminal[4 * a + b] + p.q_terminal[4 * b + a]);
     }
-  constexpr int CW = S::CW;
+  // the cost weights are diagonal in the default parameters (a uniform branch)
+  bool diag = true;
 #pragma unroll
-  for (int c = 0; c < CW; ++c) C.r[c] = 0.0;
-  auto column = [&](int col, bool gcol, bool keep) {
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int b = 0; b < 4; ++b)
+      if (a != b) diag = diag && p.q[4 * a + b] == 0.0 && p.q_terminal[4 * a + b] == 0.0;
+  constexpr int CW = S::CW;
+  constexpr int kHS = CW / 2;  // steps per part: part h holds the rows of the steps h kHS + 1 .. h kHS + kHS
+  const int hu = __builtin_amdgcn_readfirstlane(C.h);
+  const int wpu = __builtin_amdgcn_readfirstlane(C.w % S::kRW);
+  // the gradient column: row n of every part (a padding row, its part's rows in r[] like a variable
+  // column, stored to sm.g after the pass), or, when the rows fill the row waves (n = kNX), a second
+  // wave-uniform pass on the last part's first row wave that stores sm.g per step
+  const bool g_lane = n < S::kNX && i == n;
+  const bool g_pass = n == S::kNX && hu == S::kParts - 1 && wpu == 0;  // uniform
+  // Straight-line code per part block (one uniform branch per block), so the scheduler pipelines the
+  // steps' LDS reads: the mid buckets hold N >= NT - 7, so only the top 8 steps can lie past N or be
+  // the terminal one, and those select instead of branching.
+  static_assert(kHS >= 8, "the top 8 steps lie in the last part's block");
+  auto recursion = [&](auto is_diag, auto is_gpass, bool gcol, int col, int hlo) {
+    constexpr bool kDiag = decltype(is_diag)::value;
+    constexpr bool kGPass = decltype(is_gpass)::value;  // second pass: the gradient column, stored per step
     const int j = col >> 1;
-    const int ccol = col & 1;
-    const double sj = gcol ? 0.0 : si[j];
+    const int cc = col & 1;
+    const double sj = gcol ? 1.0 : si[j];
     const double pa0 = gcol ? 0.0 : sm.pre[0][j + 1], pg0 = gcol ? 0.0 : sm.pre[2][j + 1];
     const double bj = (!gcol && j + 1 < N) ? be[j + 1] : 0.0, ej = (!gcol && j + 1 < N) ? et[j + 1] : 0.0;
+    const bool st = gcol || cc == 1;  // s0 / s1 from the prefix sums (or e_m)
+    const double k01 = st ? sj : 0.0, o0 = st ? pa0 : 0.0, o1 = st ? pg0 : 0.0;
+    const double b0 = st ? 0.0 : bj, b1 = st ? 0.0 : ej;
+    const double kg = gcol ? 1.0 : 0.0;
+    const double c2v = (!gcol && cc == 1) ? sj : 0.0;
+    // thresholds: s0 / s1 live for m > t01, s2 for m > t2, s3 == 1 at m == t3
+    const int t01 = gcol ? 0 : (cc == 1 ? j : j + 1);
+    const int t2 = gcol ? 0 : j;
+    const int t3 = (!gcol && cc == 0) ? j + 1 : -1;
+    const double* X0 = gcol ? sm.err[0] : sm.pre[0];
+    const double* X1 = gcol ? sm.err[1] : sm.pre[2];
+    const double* X2 = gcol ? sm.err[2] : sm.pre[0];  // kg = 0: read, not used
+    const double* X3 = gcol ? sm.err[3] : sm.pre[0];
     double mu0 = 0.0, mu1 = 0.0, mu2 = 0.0;
-    Unroll<0, NT>::run([&](auto mc) {
-      constexpr int m = NT - decltype(mc)::value;  // NT .. 1
-      if (m <= N) {
-        double s0, s1, s2, s3;
-        if (gcol) {
-          s0 = sm.err[m][0];
-          s1 = sm.err[m][1];
-          s2 = sm.err[m][2];
-          s3 = sm.err[m][3];
-        } else if (m > j) {
-          if (ccol == 0) {
-            s0 = m >= j + 2 ? bj : 0.0;
-            s1 = m >= j + 2 ? ej : 0.0;
-            s2 = 0.0;
-            s3 = m == j + 1 ? 1.0 : 0.0;
-          } else {
-            s0 = sj * (sm.pre[0][m] - pa0);
-            s1 = sj * (sm.pre[2][m] - pg0);
-            s2 = sj;
-            s3 = 0.0;
-          }
-        } else {
-          s0 = s1 = s2 = s3 = 0.0;
-        }
-        const bool term = m == N;
-        auto Wm = [&](int a, int k) -> double { return term ? QN[a][k] : Q[a][k]; };
-        const double w0 = Wm(0, 0) * s0 + Wm(0, 1) * s1 + Wm(0, 2) * s2 + Wm(0, 3) * s3;
-        const double w1 = Wm(1, 0) * s0 + Wm(1, 1) * s1 + Wm(1, 2) * s2 + Wm(1, 3) * s3;
-        const double w2 = Wm(2, 0) * s0 + Wm(2, 1) * s1 + Wm(2, 2) * s2 + Wm(2, 3) * s3;
-        const double w3 = Wm(3, 0) * s0 + Wm(3, 1) * s1 + Wm(3, 2) * s2 + Wm(3, 3) * s3;
-        double ha;
-        if (!term) {
-          const double m0 = mu0, m1 = mu1;
-          ha = w3 + (be[m] * m0 + et[m] * m1);
-          mu0 = w0 + m0;
-          mu1 = w1 + m1;
-          mu2 = w2 + (mu2 + al[m] * m0 + ga[m] * m1);
-        } else {
-          ha = w3;
-          mu0 = w0;
-          mu1 = w1;
-          mu2 = w2;
-        }
-        const double hd = si[m - 1] * mu2;
-        constexpr int row0 = 2 * (m - 1);
-        if (gcol) {
+    auto step = [&](auto mcst) {
+      constexpr int m = decltype(mcst)::value;
+      constexpr bool kTop = m > NT - 8;  // may be past N (skipped: selects keep the state) or terminal
+      const bool on = !kTop || m <= N;
+      const bool term = kTop && m == N;
+      double s0 = fma(k01, X0[m] - o0, b0);
+      double s1 = fma(k01, X1[m] - o1, b1);
+      s0 = m > t01 ? s0 : 0.0;
+      s1 = m > t01 ? s1 : 0.0;
+      const double s2 = fma(kg, X2[m], m > t2 ? c2v : 0.0);
+      const double s3 = fma(kg, X3[m], m == t3 ? 1.0 : 0.0);
+      auto Wm = [&](int a, int k) -> double {
+        if constexpr (kTop)
+          return term ? QN[a][k] : Q[a][k];
+        else
+          return Q[a][k];
+      };
+      double w0, w1, w2, w3;
+      if constexpr (kDiag) {
+        w0 = Wm(0, 0) * s0;
+        w1 = Wm(1, 1) * s1;
+        w2 = Wm(2, 2) * s2;
+        w3 = Wm(3, 3) * s3;
+      } else {
+        w0 = Wm(0, 0) * s0 + Wm(0, 1) * s1 + Wm(0, 2) * s2 + Wm(0, 3) * s3;
+        w1 = Wm(1, 0) * s0 + Wm(1, 1) * s1 + Wm(1, 2) * s2 + Wm(1, 3) * s3;
+        w2 = Wm(2, 0) * s0 + Wm(2, 1) * s1 + Wm(2, 2) * s2 + Wm(2, 3) * s3;
+        w3 = Wm(3, 0) * s0 + Wm(3, 1) * s1 + Wm(3, 2) * s2 + Wm(3, 3) * s3;
+      }
+      const double m0 = mu0, m1 = mu1;
+      double ha = w3 + (be[m] * m0 + et[m] * m1);
+      double n0 = w0 + m0;
+      double n1 = w1 + m1;
+      double n2 = w2 + (mu2 + al[m] * m0 + ga[m] * m1);
+      if constexpr (kTop) {  // the terminal step starts the recursion; steps past N leave it at zero
+        ha = term ? w3 : ha;
+        n0 = term ? w0 : n0;
+        n1 = term ? w1 : n1;
+        n2 = term ? w2 : n2;
+        mu0 = on ? n0 : mu0;
+        mu1 = on ? n1 : mu1;
+        mu2 = on ? n2 : mu2;
+      } else {
+        mu0 = n0;
+        mu1 = n1;
+        mu2 = n2;
+      }
+      const double hd = si[m - 1] * mu2;
+      constexpr int row0 = 2 * (m - 1);
+      if constexpr (kGPass) {
+        if (on) {
           sm.g[row0] = ha;
           sm.g[row0 + 1] = hd;
-        } else if (keep) {  // rows row0, row0 + 1 (same part: CW is even)
-          if (C.h == row0 / CW) {
-            C.r[row0 % CW] = ha;
-            C.r[row0 % CW + 1] = hd;
-          }
         }
+      } else {
+        // rows row0, row0 + 1 of the step's part (CW is even); this block runs only on that part's
+        // waves and the ones below it, so the store is a uniform test of the part
+        if (hu == row0 / CW) {
+          C.r[row0 % CW] = on ? ha : C.r[row0 % CW];
+          C.r[row0 % CW + 1] = on ? hd : C.r[row0 % CW + 1];
+        }
+      }
+    };
+    Unroll<0, S::kParts>::run([&](auto bc) {
+      constexpr int blk = S::kParts - 1 - decltype(bc)::value;  // the part whose steps these are
+      if (blk >= hlo) {
+        Unroll<0, kHS>::run([&](auto tc) {
+          step(std::integral_constant<int, blk * kHS + kHS - decltype(tc)::value>{});
+        });
       }
     });
   };
-  if (act) column(i, false, true);
-  // the gradient column: a padding row of the h = 0 half, or (2N = NP) row 0 of the h = 1 half
-  const bool gthread = n < S::NP ? (C.h == 0 && i == n) : (C.h == 1 && i == 0);
-  if (gthread) column(0, true, false);
+  {
+    // first pass: every lane; inactive rows take column 0's constants and are zeroed below.  The rows
+    // of the steps past N (N < NT) are not written: zeros.
+#pragma unroll
+    for (int c = 0; c < CW; ++c) C.r[c] = 0.0;
+    if (diag)
+      recursion(std::true_type{}, std::false_type{}, g_lane, act ? i : 0, hu);
+    else
+      recursion(std::false_type{}, std::false_type{}, g_lane, act ? i : 0, hu);
+    if (g_lane)
+#pragma unroll
+      for (int c = 0; c < CW; ++c) sm.g[hu * CW + c] = C.r[c];
+    if (!act)
+#pragma unroll
+      for (int c = 0; c < CW; ++c) C.r[c] = 0.0;
+    if constexpr (S::NP == S::kNX) {
+      if (g_pass) {  // n = kNX: the gradient column as a second, wave-uniform pass
+        if (diag)
+          recursion(std::true_type{}, std::true_type{}, true, 0, 0);
+        else
+          recursion(std::false_type{}, std::true_type{}, true, 0, 0);
+      }
+    }
+  }
+  const bool gthread = (g_lane && hu == 0) || (g_pass && C.lane == 0);
   __syncthreads();
-  // input cost sum_k U_k' R U_k with a_k = (v_{k+1} - v_k)/dt: a band of column i
-  const double r00 = 0.5 * (p.r[0] + p.r[0]) / (dt * dt), r10 = 0.5 * (p.r[2] + p.r[1]) / dt;
-  const double r11 = 0.5 * (p.r[3] + p.r[3]);
+  C.T.mark(10);
+  // input cost sum_k U_k' R U_k with a_k = (v_{k+1} - v_k)/dt: a band of column i, read from the band
+  // table at offset col - i (above)
   if (gthread) {
     sm.g[0] += -x0[3] * r00;
     sm.g[1] += -x0[3] * r10;
   }
   if (act) {
+    const int kind = cc == 1 ? 2 : (i + 2 < n ? 0 : 1);
+    const double* tb = bt + kind * (2 * S::kNX) + S::kNX + hu * CW - i;
 #pragma unroll
-    for (int c = 0; c < CW; ++c) {
-      const int d = C.h * CW + c - i;
-      double add = 0.0;
-      if (cc == 0) {
-        if (d == 0) add = i + 2 < n ? 2.0 * r00 : r00;
-        if (d == 2 || d == -2) add = -r00;
-        if (d == 1) add = r10;
-        if (d == 3) add = -r10;
-      } else {
-        if (d == 0) add = r11;
-        if (d == -1) add = r10;
-        if (d == -3) add = -r10;
-      }
-      C.r[c] += add;
-    }
+    for (int c = 0; c < CW; ++c) C.r[c] += tb[c];
   }
   __syncthreads();
 
@@ -734,6 +852,7 @@ __device__ __forceinline__ bool mid_setup(const mpcqp_params& p, Mid<NT>& C) {
     return V && act ? v : 0.0;
   };
   double cmax = rowmax(cmx);
+  C.T.mark(11);
   double lo[3], hi[3], wt[3], E[3];
   const double idt = 1.0 / dt, v0 = x0[3];
   double k1[2], k2[3];
@@ -813,6 +932,7 @@ __device__ __forceinline__ bool mid_setup(const mpcqp_params& p, Mid<NT>& C) {
   }
 #pragma unroll
   for (int c = 0; c < CW; ++c) C.r[c] *= cpend;
+  C.T.mark(12);
   // Pbar to the workspace (every row, padding zeros included)
   {
     double* pc = C.Pg + (size_t)(C.h * CW) * kMidLD + i;
@@ -823,6 +943,7 @@ __device__ __forceinline__ bool mid_setup(const mpcqp_params& p, Mid<NT>& C) {
       fin = fin && isfinite(C.r[c]);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    C.T.mark(13);
     bool finite = fin && isfinite(qv) && isfinite(cscale);
     double wb[3];
 #pragma unroll
@@ -861,6 +982,7 @@ __device__ __forceinline__ bool mid_setup(const mpcqp_params& p, Mid<NT>& C) {
       sm.cf[5][i] = C.c22;
     }
     __syncthreads();
+    C.T.mark(14);
     return bad;
   }
 }

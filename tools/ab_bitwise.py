@@ -32,6 +32,10 @@ MID_CASES = [  # the mid-horizon kernel (N = 33..64)
     ("config3", 56, 512, "auto", {}),
     ("config3", 64, 512, "auto", {}),
     ("config3", 40, 512, "auto", {"max_iter": 40, "polish": 0}),
+    ("config3", 37, 512, "auto", {}),  # N < NT: padding steps in every bucket
+    ("config3", 45, 512, "auto", {}),
+    ("config3", 53, 256, "auto", {}),
+    ("config3", 61, 256, "auto", {}),
 ]
 if os.environ.get("MPCQP_AB_MID") == "1":
     CASES = MID_CASES

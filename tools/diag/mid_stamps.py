@@ -15,6 +15,9 @@ ROOT = Path(__file__).resolve().parents[2]
 DIAG = ROOT / "tools" / "diag"
 LIB = DIAG / "libmpcqp_midstamps.so"
 PHASES = ["setup", "admm_fact", "admm_iter", "admm_check", "polish_fact", "polish_total", "outputs", "qp_total"]
+# the setup's sub-phases (slots 9..14 of the stamp buffer)
+SETUP = {9: "s_prefix_free_response", 10: "s_condense", 11: "s_input_band_rowmax", 12: "s_ruiz",
+         13: "s_pbar_store", 14: "s_rest"}
 
 
 def build():
@@ -24,6 +27,7 @@ def build():
     g.HIPCC_FLAGS = g.HIPCC_FLAGS + ["-DMPCQP_MID_STAMPS"]
     g.OBJ_DIR = DIAG / "obj_midstamps"
     g.LIB = LIB
+    g.library_build_id.__defaults__ = (LIB,)  # its default was bound to the product library
     g.RESOURCES = DIAG / "obj_midstamps" / "resources.json"
     g.build_library()
     print("built", LIB)
@@ -53,7 +57,8 @@ def run(Ns):
         fn(buf, 1)
         q = max(1, buf[8])
         it = ctrl._iters[:4096].cpu().numpy().mean(axis=0).tolist()
-        out[f"N{N}"] = {"qps": q, **{k: buf[i] / q for i, k in enumerate(PHASES)}, "iters_mean": it}
+        out[f"N{N}"] = {"qps": q, **{k: buf[i] / q for i, k in enumerate(PHASES)},
+                        **{k: buf[i] / q for i, k in SETUP.items()}, "iters_mean": it}
         ctrl.close()
     print(json.dumps(out, indent=1))
 
