@@ -27,13 +27,15 @@ constexpr int kMidLD = 128;  // row stride (doubles) of the workspace Pbar
 // Diagnostic builds only (-DMPCQP_MID_STAMPS, never the measured library): per-phase s_memtime sums of
 // each QP's thread 0, added into g_mid_stamps[] at the end (read by mpcqp_debug_mid_stamps_<NT>).
 #ifdef MPCQP_MID_STAMPS
-__device__ unsigned long long g_mid_stamps[16];
+constexpr int kMidStampSlots = 24;
+__device__ unsigned long long g_mid_stamps[kMidStampSlots];
 struct MidStamps {
-  // 0..7 the phases, 9..15 the setup's sub-phases (mark()); g_mid_stamps[8] counts the QPs
-  unsigned long long acc[16] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+  // 0..7 the phases, 9..14 the setup's sub-phases and 16..20 the polish's (mark()); [8] counts the QPs
+  unsigned long long acc[kMidStampSlots] = {};
   unsigned long long t = 0, t2 = 0;
   __device__ __forceinline__ void begin() { t = t2 = __builtin_amdgcn_s_memtime(); }
   __device__ __forceinline__ void end(int k) { acc[k] += __builtin_amdgcn_s_memtime() - t; }
+  __device__ __forceinline__ void mbegin() { t2 = __builtin_amdgcn_s_memtime(); }
   __device__ __forceinline__ void mark(int k) {
     const unsigned long long now = __builtin_amdgcn_s_memtime();
     acc[k] += now - t2;
@@ -41,7 +43,7 @@ struct MidStamps {
   }
   __device__ __forceinline__ void flush() {
     if (threadIdx.x == 0) {
-      for (int k = 0; k < 16; ++k)
+      for (int k = 0; k < kMidStampSlots; ++k)
         if (k != 8) atomicAdd(&g_mid_stamps[k], acc[k]);
       atomicAdd(&g_mid_stamps[8], 1ull);
     }
@@ -51,6 +53,7 @@ struct MidStamps {
 struct MidStamps {
   __device__ __forceinline__ void begin() {}
   __device__ __forceinline__ void end(int) {}
+  __device__ __forceinline__ void mbegin() {}
   __device__ __forceinline__ void mark(int) {}
   __device__ __forceinline__ void flush() {}
 };
@@ -279,8 +282,10 @@ struct Mid {
   //   3. the V threads add the parts' sums of their row AND of the rows 2 and 4 back (the same sums in
   //      the same order as the owners'), which is all Cbar xa needs.
   // xa and za (= Cbar xa) on V threads.
+  // The soft rows' bounds are loaded just before the second barrier (for the projection after it): their LDS
+  // round trip hides in the barrier's wait, where few registers are live.
   __device__ __forceinline__ void admm_linear(const double tmp[3], double sg, double x, double alpha, double& xa,
-                                              double za[3]) {
+                                              double za[3], double lo_[3], double hi_[3]) {
     if (V) {
       sm->abx[0][i] = c11 * tmp[1] + c21 * tmp[2];  // to the variable 2 back
       sm->abx[1][i] = c22 * tmp[2];                 // to the variable 4 back
@@ -303,6 +308,11 @@ struct Mid {
       fmac_bc<c % 16>(a[c % 4], w[c / 16], r[c]);
     });
     sm->tr[h][0][i] = (a[0] + a[1]) + (a[2] + a[3]);
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      lo_[k] = V ? LO(k) : 0.0;
+      hi_[k] = V ? HI(k) : 0.0;
+    }
     sync();
     if (V) {
       auto xa_of = [&](int row) -> double {  // combine's sum, inv_mul's sign, alpha
@@ -1011,6 +1021,7 @@ __device__ __forceinline__ int mid_polish(Mid<NT>& C, double& x, const double zg
       rw[k] = cd[k] ? 2.0 * C.WB(k) : 0.0;
       tmp[k] = cd[k] == 2 ? rw[k] * C.HI(k) : (cd[k] == 1 ? rw[k] * C.LO(k) : 0.0);
     }
+    C.T.mbegin();
     bool refac = !have_fact;
     if (!refac) {
       // changed soft rows: each row wave's ballots, combined through LDS (uniform in every thread)
@@ -1046,6 +1057,7 @@ __device__ __forceinline__ int mid_polish(Mid<NT>& C, double& x, const double zg
           }
         }
     }
+    C.T.mark(16);
     if (refac) {
       C.T.begin();
       C.form(0.0, rw);
@@ -1059,6 +1071,7 @@ __device__ __forceinline__ int mid_polish(Mid<NT>& C, double& x, const double zg
       have_fact = true;
     }
     ++nfact;
+    C.T.mbegin();
 #pragma unroll
     for (int k = 0; k < 3; ++k) rwf[k] = rw[k];
     const double rhs = C.CTmul(tmp) - C.qv;
@@ -1075,7 +1088,9 @@ __device__ __forceinline__ int mid_polish(Mid<NT>& C, double& x, const double zg
       result = -1;
       break;
     }
-    if (!C.bany(diff)) {
+    const bool anyd = C.bany(diff);
+    C.T.mark(17);
+    if (!anyd) {
       double t3[3];
 #pragma unroll
       for (int k = 0; k < 3; ++k) t3[k] = rw[k] * zn[k];
@@ -1098,6 +1113,7 @@ __device__ __forceinline__ int mid_polish(Mid<NT>& C, double& x, const double zg
         break;
       }
     }
+    C.T.mark(18);
     // exact line search along d = xn - x
     double tb[3];
 #pragma unroll
@@ -1111,6 +1127,14 @@ __device__ __forceinline__ int mid_polish(Mid<NT>& C, double& x, const double zg
     double s2[2] = {act ? dx * Pd : 0.0, act ? (Px + C.qv) * dx : 0.0};
     C.template reduce<2, false>(s2);
     const double qd = s2[0], lin = s2[1];
+    // the soft rows' bounds and weights in registers for the trials (LDS round trips per use otherwise)
+    double lo_[3], hi_[3], wb2[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      lo_[k] = C.LO(k);
+      hi_[k] = C.HI(k);
+      wb2[k] = 2.0 * C.WB(k);
+    }
     double t = 1.0;
     for (int ls = 0; ls < 40; ++ls) {
       ++n_ls;
@@ -1118,9 +1142,9 @@ __device__ __forceinline__ int mid_polish(Mid<NT>& C, double& x, const double zg
 #pragma unroll
       for (int k = 0; k < 3; ++k) {
         const double zt = zc[k] + t * zd[k];
-        const double rr = zt > C.HI(k) ? zt - C.HI(k) : (zt < C.LO(k) ? zt - C.LO(k) : 0.0);
-        g12[0] += 2.0 * C.WB(k) * rr * zd[k];
-        if (rr != 0.0) g12[1] += 2.0 * C.WB(k) * zd[k] * zd[k];
+        const double rr = zt > hi_[k] ? zt - hi_[k] : (zt < lo_[k] ? zt - lo_[k] : 0.0);
+        g12[0] += wb2[k] * rr * zd[k];
+        if (rr != 0.0) g12[1] += wb2[k] * zd[k] * zd[k];
       }
       if (!C.V) g12[0] = g12[1] = 0.0;
       C.template reduce<2, false>(g12);
@@ -1133,16 +1157,18 @@ __device__ __forceinline__ int mid_polish(Mid<NT>& C, double& x, const double zg
 #pragma unroll
       for (int k = 0; k < 3; ++k) {
         const double za = zc[k] + t * zd[k], zb = zc[k] + tn * zd[k];
-        const int ca = za > C.HI(k) ? 2 : (za < C.LO(k) ? 1 : 0);
-        const int cb = zb > C.HI(k) ? 2 : (zb < C.LO(k) ? 1 : 0);
+        const int ca = za > hi_[k] ? 2 : (za < lo_[k] ? 1 : 0);
+        const int cb = zb > hi_[k] ? 2 : (zb < lo_[k] ? 1 : 0);
         moved = moved || ca != cb;
       }
       t = tn;
       if (!C.bany(C.V && moved)) break;
     }
+    C.T.mark(19);
     x = x + t * dx;
     Px = Px + t * Pd;
     C.Cmul(x, zc);
+    C.T.mark(20);
 #pragma unroll
     for (int k = 0; k < 3; ++k) cd[k] = zc[k] > C.HI(k) ? 2 : (zc[k] < C.LO(k) ? 1 : 0);
   }
@@ -1194,14 +1220,14 @@ __device__ __forceinline__ int mid_admm(const mpcqp_params& p, Mid<NT>& C, MidAd
       double tmp[3];
 #pragma unroll
       for (int k = 0; k < 3; ++k) tmp[k] = rho * S.z[k] - S.y[k];
-      double xa, za[3];
-      C.admm_linear(tmp, sg, S.x, alpha, xa, za);
+      double xa, za[3], lo_[3], hi_[3];
+      C.admm_linear(tmp, sg, S.x, alpha, xa, za, lo_, hi_);
       S.x = xa + oma * S.x;
 #pragma unroll
       for (int k = 0; k < 3; ++k) {
         const double v = za[k] + oma * S.z[k];
         const double vv = v + S.y[k] * ir;
-        const double d = vv - min_nc(max_nc(vv, C.LO(k)), C.HI(k));
+        const double d = vv - min_nc(max_nc(vv, lo_[k]), hi_[k]);
         S.z[k] = vv - pb[k] * d;
         S.y[k] = rpb[k] * d;
       }
@@ -1536,11 +1562,11 @@ template void launch_solve_mid<MPCQP_MID_PART>(hipStream_t, const Launch&);
 #ifdef MPCQP_MID_STAMPS
 #define MPCQP_CAT2(a, b) a##b
 #define MPCQP_CAT(a, b) MPCQP_CAT2(a, b)
-extern "C" int MPCQP_CAT(mpcqp_debug_mid_stamps_, MPCQP_MID_PART)(unsigned long long* out16, int reset) {
+extern "C" int MPCQP_CAT(mpcqp_debug_mid_stamps_, MPCQP_MID_PART)(unsigned long long* out, int reset) {
   hipError_t e = hipDeviceSynchronize();
-  if (e == hipSuccess && out16) e = hipMemcpyFromSymbol(out16, HIP_SYMBOL(g_mid_stamps), sizeof(unsigned long long) * 16);
+  if (e == hipSuccess && out) e = hipMemcpyFromSymbol(out, HIP_SYMBOL(g_mid_stamps), sizeof(unsigned long long) * kMidStampSlots);
   if (e == hipSuccess && reset) {
-    unsigned long long z[16] = {0};
+    unsigned long long z[kMidStampSlots] = {0};
     e = hipMemcpyToSymbol(HIP_SYMBOL(g_mid_stamps), z, sizeof(z));
   }
   return e == hipSuccess ? 0 : -4;

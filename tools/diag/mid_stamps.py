@@ -17,7 +17,8 @@ LIB = DIAG / "libmpcqp_midstamps.so"
 PHASES = ["setup", "admm_fact", "admm_iter", "admm_check", "polish_fact", "polish_total", "outputs", "qp_total"]
 # the setup's sub-phases (slots 9..14 of the stamp buffer)
 SETUP = {9: "s_prefix_free_response", 10: "s_condense", 11: "s_input_band_rowmax", 12: "s_ruiz",
-         13: "s_pbar_store", 14: "s_rest"}
+         13: "s_pbar_store", 14: "s_rest",
+         16: "p_ballot_rank1", 17: "p_solve", 18: "p_refine", 19: "p_line_search", 20: "p_step"}
 
 
 def build():
@@ -46,7 +47,7 @@ def run(Ns):
     for N in Ns:
         b = scenarios.config3(4096, horizon=N)
         ctrl = BatchedMPCController(MPCConfig(horizon=N).to_parameters(0.8), 4096, device="cuda:0")
-        buf = (ctypes.c_ulonglong * 16)()
+        buf = (ctypes.c_ulonglong * 24)()
         nt = 32 if N <= 32 else (40 if N <= 40 else (48 if N <= 48 else (56 if N <= 56 else 64)))
         fn = getattr(L, f"mpcqp_debug_mid_stamps_{nt}")
         ctrl.solve_batch(b.x0, b.ref, b.u_prev)
