@@ -236,6 +236,15 @@ struct Mid {
     z[1] = c10 * x + c11 * xm2;
     z[2] = (c20 * x + c21 * xm2) + c22 * xm4;
   }
+  // ... and the soft rows' bounds, loaded ahead of the exchange's barrier (their round trip hides there)
+  __device__ __forceinline__ void Cmul(double x, double z[3], double lo_[3], double hi_[3]) {
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      lo_[k] = V ? LO(k) : 0.0;
+      hi_[k] = V ? HI(k) : 0.0;
+    }
+    Cmul(x, z);
+  }
   // x = Cbar' y: own rows' terms, the terms for the variable 2 back (a) and 4 back (b) of rows 2 / 4
   // ahead -- t + (a[i + 2] + b[i + 4]), the one-wave kernel's shl2(a + shl2(b))
   __device__ __forceinline__ double CTmul(const double y[3]) {
@@ -629,10 +638,14 @@ __device__ __forceinline__ bool mid_setup(const mpcqp_params& p, Mid<NT>& C) {
         },
         [&](auto kc, const Rq& v) {
           constexpr int k = decltype(kc)::value;
-          if (k < N) {
-            acc = acc + v.a * h + (k == 0 ? b0 : 0.0) * (k == 0 ? v0 : 0.0) + one * v.c;
-            out[k + 1] = acc - one * v.r;
-          }
+          // straight-line: the steps past N (only the top 8: N >= NT - 7) keep acc and write rows the
+          // condensing reads only into discarded selects
+          const double an = acc + v.a * h + (k == 0 ? b0 : 0.0) * (k == 0 ? v0 : 0.0) + one * v.c;
+          if constexpr (k >= NT - 8)
+            acc = k < N ? an : acc;
+          else
+            acc = an;
+          out[k + 1] = acc - one * v.r;
         });
   } else if (tid >= kWave && tid < kWave + N) {
     const int m = tid - kWave + 1;
@@ -1005,10 +1018,13 @@ __device__ __forceinline__ int mid_polish(Mid<NT>& C, double& x, const double zg
   int result = 0;
   double zc[3];
   int cd[3];
-  C.Cmul(x, zc);
-  double Px = C.Pmul(x);
+  {
+    double lo_[3], hi_[3];
+    C.Cmul(x, zc, lo_, hi_);
 #pragma unroll
-  for (int k = 0; k < 3; ++k) cd[k] = zg[k] > C.HI(k) ? 2 : (zg[k] < C.LO(k) ? 1 : 0);
+    for (int k = 0; k < 3; ++k) cd[k] = zg[k] > hi_[k] ? 2 : (zg[k] < lo_[k] ? 1 : 0);
+  }
+  double Px = C.Pmul(x);
   const int kMaxRank1 = C.n / 2;
   double rwf[3] = {0.0, 0.0, 0.0};
   bool have_fact = false;
@@ -1076,12 +1092,12 @@ __device__ __forceinline__ int mid_polish(Mid<NT>& C, double& x, const double zg
     for (int k = 0; k < 3; ++k) rwf[k] = rw[k];
     const double rhs = C.CTmul(tmp) - C.qv;
     double xn = C.inv_mul(rhs);
-    double zn[3];
-    C.Cmul(xn, zn);
+    double zn[3], lo_[3], hi_[3];
+    C.Cmul(xn, zn, lo_, hi_);
     bool diff = false;
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
-      const int c2 = zn[k] > C.HI(k) ? 2 : (zn[k] < C.LO(k) ? 1 : 0);
+      const int c2 = zn[k] > hi_[k] ? 2 : (zn[k] < lo_[k] ? 1 : 0);
       diff = diff || (c2 != cd[k]);
     }
     if (C.bany(!isfinite(xn))) {
@@ -1100,7 +1116,7 @@ __device__ __forceinline__ int mid_polish(Mid<NT>& C, double& x, const double zg
       diff = false;
 #pragma unroll
       for (int k = 0; k < 3; ++k) {
-        const int c2 = zn[k] > C.HI(k) ? 2 : (zn[k] < C.LO(k) ? 1 : 0);
+        const int c2 = zn[k] > hi_[k] ? 2 : (zn[k] < lo_[k] ? 1 : 0);
         diff = diff || (c2 != cd[k]);
       }
       if (C.bany(!isfinite(xn))) {
@@ -1117,7 +1133,7 @@ __device__ __forceinline__ int mid_polish(Mid<NT>& C, double& x, const double zg
     // exact line search along d = xn - x
     double tb[3];
 #pragma unroll
-    for (int k = 0; k < 3; ++k) tb[k] = rw[k] * (zn[k] - (cd[k] == 2 ? C.HI(k) : (cd[k] == 1 ? C.LO(k) : 0.0)));
+    for (int k = 0; k < 3; ++k) tb[k] = rw[k] * (zn[k] - (cd[k] == 2 ? hi_[k] : (cd[k] == 1 ? lo_[k] : 0.0)));
     const double ctb = C.CTmul(tb);
     const double dx = act ? xn - x : 0.0;
     const double Pd = act ? (-ctb - C.qv) - Px : 0.0;
@@ -1127,14 +1143,10 @@ __device__ __forceinline__ int mid_polish(Mid<NT>& C, double& x, const double zg
     double s2[2] = {act ? dx * Pd : 0.0, act ? (Px + C.qv) * dx : 0.0};
     C.template reduce<2, false>(s2);
     const double qd = s2[0], lin = s2[1];
-    // the soft rows' bounds and weights in registers for the trials (LDS round trips per use otherwise)
-    double lo_[3], hi_[3], wb2[3];
+    // the soft rows' bounds (above) and weights in registers for the trials (LDS round trips per use otherwise)
+    double wb2[3];
 #pragma unroll
-    for (int k = 0; k < 3; ++k) {
-      lo_[k] = C.LO(k);
-      hi_[k] = C.HI(k);
-      wb2[k] = 2.0 * C.WB(k);
-    }
+    for (int k = 0; k < 3; ++k) wb2[k] = 2.0 * C.WB(k);
     double t = 1.0;
     for (int ls = 0; ls < 40; ++ls) {
       ++n_ls;
@@ -1170,7 +1182,7 @@ __device__ __forceinline__ int mid_polish(Mid<NT>& C, double& x, const double zg
     C.Cmul(x, zc);
     C.T.mark(20);
 #pragma unroll
-    for (int k = 0; k < 3; ++k) cd[k] = zc[k] > C.HI(k) ? 2 : (zc[k] < C.LO(k) ? 1 : 0);
+    for (int k = 0; k < 3; ++k) cd[k] = zc[k] > hi_[k] ? 2 : (zc[k] < lo_[k] ? 1 : 0);
   }
   return result;
 }
