@@ -60,6 +60,16 @@ struct MidStamps {
 #endif
 constexpr int kMidWaves = 2;  // waves per SIMD the register allocation targets
 
+// The workgroup barrier of this kernel, LDS-only: every cross-wave exchange goes through LDS, and the
+// workspace entries a thread reads (its row of Pbar) are its own, ordered by the hardware, so a barrier
+// need not wait for the outstanding global stores (the Pbar store of the setup, the band's
+// read-modify-write in form()) as __syncthreads() would.
+__device__ __forceinline__ void mid_barrier() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
 // f(c, ld(c)) for c in [0, NT), the loads issued one group of G ahead of their uses and no further
 // (a scheduling barrier per group): the operand column never occupies more than 2 G registers next to
 // the NT doubles of the row (hoisting every load ahead of the FMAs spills the row).
@@ -157,7 +167,7 @@ struct Mid {
   MidStamps T;  // phases: 0 setup, 1 ADMM factorizations, 2 ADMM iterations, 3 termination checks,
                 // 4 polish factorizations / rank-1 updates, 5 polish rest, 6 outputs, 7 whole QP
 
-  __device__ __forceinline__ static void sync() { __syncthreads(); }
+  __device__ __forceinline__ static void sync() { mid_barrier(); }
 
   // The CW values v[h CW + c] (c < CW) of an LDS vector, in every lane for the fmac_bc products: lane
   // l loads element h CW + l (one conflict-free per-lane read) and the permlane broadcast (bcast,
@@ -410,17 +420,15 @@ struct Mid {
 #pragma unroll
     for (int d = 0; d < 5; ++d)
       if (own[d]) Pg[addr[d]] = orig[d] + sm->band[d][ii];
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    // (same-thread accesses to the same addresses: the hardware keeps them in order, no waits)
     const double* pc = Pg + (size_t)(h * CW) * kMidLD + ii;
     Unroll<0, CW>::run([&](auto cc) {
       constexpr int c = decltype(cc)::value;
       r[c] = pc[(size_t)c * kMidLD];
     });
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #pragma unroll
     for (int d = 0; d < 5; ++d)
       if (own[d]) Pg[addr[d]] = orig[d];
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
 
   // Symmetric sweep on the rows in r[], pivots in pairs K = {k, k + 1} (n is even): afterwards A^{-1} = -r.
@@ -674,7 +682,7 @@ __device__ __forceinline__ bool mid_setup(const mpcqp_params& p, Mid<NT>& C) {
     }
     bt[e] = v;
   }
-  __syncthreads();
+  mid_barrier();
   C.T.mark(9);
 
   // ---- condense: column i of H by the backward adjoint recursion, the rows of this thread's part into
@@ -836,7 +844,7 @@ __device__ __forceinline__ bool mid_setup(const mpcqp_params& p, Mid<NT>& C) {
     }
   }
   const bool gthread = (g_lane && hu == 0) || (g_pass && C.lane == 0);
-  __syncthreads();
+  mid_barrier();
   C.T.mark(10);
   // input cost sum_k U_k' R U_k with a_k = (v_{k+1} - v_k)/dt: a band of column i, read from the band
   // table at offset col - i (above)
@@ -850,7 +858,7 @@ __device__ __forceinline__ bool mid_setup(const mpcqp_params& p, Mid<NT>& C) {
 #pragma unroll
     for (int c = 0; c < CW; ++c) C.r[c] += tb[c];
   }
-  __syncthreads();
+  mid_barrier();
 
   // ---- unscaled data: P = 2H, q = 2g, folded row bounds (V threads: one variable per row)
   double qv = V && act ? 2.0 * sm.g[i] : 0.0;
@@ -864,14 +872,14 @@ __device__ __forceinline__ bool mid_setup(const mpcqp_params& p, Mid<NT>& C) {
   auto rowmax = [&](const double* cm4) -> double {
     double v = fmax(fmax(cm4[0], cm4[1]), fmax(cm4[2], cm4[3]));
     if (!V) sm.pp[C.h - 1][i] = v;
-    __syncthreads();
+    mid_barrier();
     if (V) {
       if constexpr (S::kParts == 2)
         v = fmax(v, sm.pp[0][i]);
       else
         v = fmax(fmax(v, sm.pp[0][i]), fmax(sm.pp[1][i], sm.pp[2][i]));
     }
-    __syncthreads();
+    mid_barrier();
     return V && act ? v : 0.0;
   };
   double cmax = rowmax(cmx);
@@ -928,7 +936,7 @@ __device__ __forceinline__ bool mid_setup(const mpcqp_params& p, Mid<NT>& C) {
     const double el2 = va ? rsqrt(limit_scaling(E[2] * r2)) : 0.0;
     // P <- ct_prev dl P dl: the row's factor and the half's column factors from LDS
     if (V) sm.vec[i] = dl;
-    __syncthreads();
+    mid_barrier();
     const double dlc = sm.vec[i] * cpend;
     const double* dj = sm.vec + C.h * CW;
     double cmp[4] = {0.0, 0.0, 0.0, 0.0};
@@ -965,7 +973,6 @@ __device__ __forceinline__ bool mid_setup(const mpcqp_params& p, Mid<NT>& C) {
       pc[(size_t)c * kMidLD] = C.r[c];
       fin = fin && isfinite(C.r[c]);
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     C.T.mark(13);
     bool finite = fin && isfinite(qv) && isfinite(cscale);
     double wb[3];
@@ -1004,7 +1011,7 @@ __device__ __forceinline__ bool mid_setup(const mpcqp_params& p, Mid<NT>& C) {
       sm.cf[4][i] = C.c21;
       sm.cf[5][i] = C.c22;
     }
-    __syncthreads();
+    mid_barrier();
     C.T.mark(14);
     return bad;
   }
@@ -1049,7 +1056,7 @@ __device__ __forceinline__ int mid_polish(Mid<NT>& C, double& x, const double zg
         if (C.V && C.lane == 0) mk[k][C.w] = b;
         if (C.V) C.sm->dw[k][C.i] = rw[k] - rwf[k];
       }
-      __syncthreads();
+      mid_barrier();
       unsigned long long chg[3][2];
       int nchg = 0;
 #pragma unroll
@@ -1355,7 +1362,7 @@ __device__ __forceinline__ void mid_finish(const mpcqp_params& p, int b, Mid<NT>
   const double* mdl = sm.model;
   const double x03 = mdl[11 * N + 7];
   if (C.V) sm.W[i] = C.act ? C.D * x : 0.0;
-  __syncthreads();
+  mid_barrier();
   const int cc = i & 1;
   if (C.V && C.act) {
     const double W = sm.W[i];
@@ -1478,7 +1485,7 @@ __global__ __launch_bounds__(MidShape<NT>::kThreads, kMidWaves) void k_solve_mid
   const int N = p.horizon;
   const double* mb = model + (size_t)b * model_stride(N);
   for (int e = tid; e < model_stride(N); e += S::kThreads) sm.model[e] = mb[e];
-  __syncthreads();
+  mid_barrier();
   MidStamps TQ;
   TQ.begin();
   C.T.begin();
