@@ -7,8 +7,8 @@ timeout -k 10 200 python bench.py --config config2 $HEAD > $O/c2.json 2> $O/c.er
 timeout -k 10 200 python bench.py --config config4 --batch 2048 $HEAD > $O/c4_b2048.json 2>> $O/c.err &&
 timeout -k 10 200 python bench.py --config config4 $HEAD > $O/c4_b16384.json 2>> $O/c.err &&
 timeout -k 10 200 python bench.py --horizon 32 $HEAD --check-sample 128 > $O/N32.json 2>> $O/c.err &&
-timeout -k 10 200 python bench.py --horizon 40 --steps 20 --warmup 10 $HEAD --check-sample 64 > $O/N40.json 2>> $O/c.err &&
-timeout -k 10 200 python bench.py --horizon 48 --steps 10 --warmup 5 $HEAD --check-sample 32 > $O/N48.json 2>> $O/c.err &&
+timeout -k 10 200 python bench.py --horizon 40 --steps 20 --warmup 20 $HEAD --check-sample 64 > $O/N40.json 2>> $O/c.err &&
+timeout -k 10 200 python bench.py --horizon 48 --steps 20 --warmup 20 $HEAD --check-sample 32 > $O/N48.json 2>> $O/c.err &&
 timeout -k 10 200 python bench.py --horizon 56 --steps 10 --warmup 5 $HEAD --check-sample 32 > $O/N56.json 2>> $O/c.err &&
 timeout -k 10 200 python bench.py --horizon 64 --steps 10 --warmup 5 $HEAD --check-sample 32 > $O/N64.json 2>> $O/c.err &&
 timeout -k 10 200 python -u tools/b1_latency.py > $O/b1_latency.json 2> $O/b1.err &&
